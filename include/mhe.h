@@ -1,0 +1,158 @@
+/*
+ * mhe.h -- C-ABI of libmhe.so, the MI355X (gfx950) batched collocation
+ * Gauss-Newton estimator.
+ *
+ * This is the drop-in boundary under the reference's solver facade:
+ *
+ *   reference                                   replaced by
+ *   ------------------------------------------  -----------------------------------
+ *   NLP.build()      nlp/nlp.py:61-69           mhe_const_bytes + mhe_build_constants
+ *   NLP.solve()      nlp/nlp.py:76-83           mhe_gn_solve  (CasADi Opti + IPOPT ->
+ *                                               hand-written HIP Gauss-Newton)
+ *   addDynamics/addDynamicsCost/addResidualCost/addInitialCost
+ *                    nlp/nlp.py:202-286         the objective those calls record is
+ *                                               what mhe_gn_solve minimises; its pieces
+ *                                               are exported for kernel-level parity:
+ *                                               mhe_assemble (J^T W J, J^T W r, cost)
+ *                                               mhe_chol_solve (dense SPD solve)
+ *   extractSolution  nlp/nlp.py:99-119          host side (Lagrange interpolation)
+ *
+ * Conventions
+ *   - every pointer argument except `dims` and the host-side constant tables
+ *     of mhe_build_constants is a DEVICE pointer owned by the caller (torch
+ *     tensors in the Python host; hipMalloc'd memory from C);
+ *   - fp64 everywhere, row-major, batch outermost; a batch stride of 0 means
+ *     "shared by every trajectory";
+ *   - no hidden allocation, no host synchronisation: every call only enqueues
+ *     work on `stream` (graph-capturable);
+ *   - returns MHE_OK (0) or a negative MHE_ERR_* code; per-trajectory solver
+ *     outcomes are reported in `status_out` (MHE_STATUS_*), never by aborting
+ *     the batch;
+ *   - calls that share a constants buffer may run concurrently on different
+ *     streams; a constants buffer is read-only after mhe_build_constants.
+ */
+#ifndef MHE_H
+#define MHE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* return codes */
+#define MHE_OK 0
+#define MHE_ERR_DIMS (-1)        /* dims inconsistent with the models / limits */
+#define MHE_ERR_MODEL (-2)       /* unknown dynamics or measurement model id   */
+#define MHE_ERR_HIP (-3)         /* a HIP runtime call failed                  */
+#define MHE_ERR_UNSUPPORTED (-4) /* valid request this build does not handle   */
+#define MHE_ERR_NULL (-5)        /* required pointer is NULL                   */
+
+/* per-trajectory solver status (status_out) */
+#define MHE_STATUS_CONVERGED 0   /* max|delta| <= tol * (1 + max|X|)           */
+#define MHE_STATUS_MAX_ITER 1    /* max_iter Gauss-Newton steps taken          */
+#define MHE_STATUS_NOT_SPD 2     /* Cholesky pivot <= 0 (J^T W J not SPD)      */
+#define MHE_STATUS_NONFINITE 3   /* NaN/Inf in the step                        */
+
+/* dynamics plug-ins (reference nlp/dynamics.py) */
+#define MHE_DYN_SINGLE_INTEGRATOR 1      /* :4-8    n=1  m=1 */
+#define MHE_DYN_SINGLE_INTEGRATOR_2D 2   /* :10-17  n=2  m=2 */
+#define MHE_DYN_SINGLE_INTEGRATOR_3D 3   /* :19-27  n=3  m=3 */
+#define MHE_DYN_DOUBLE_INTEGRATOR 4      /* :29-38  n=4  m=2 */
+#define MHE_DYN_VAN_DER_POL 5            /* :61-66  n=2  m=1 */
+#define MHE_DYN_GNSS_POS_AND_BIAS 6      /* :68-79  n=5  m=3 */
+#define MHE_DYN_MULTI_RECEIVER 7         /* :81-96  n=8  m=0 */
+#define MHE_DYN_GNSS_TWO_RECEIVER 8      /* :98-115 n=10 m=6 */
+#define MHE_DYN_KINEMATIC_BICYCLE 9      /* :117-136 n=6 m=2 (kinematic_bycicle_and_bias) */
+
+/* measurement plug-ins (reference nlp/measurements.py) */
+#define MHE_MEAS_FULL_STATE 1            /* :4-5   p=n, linear            */
+#define MHE_MEAS_PSEUDORANGE 2           /* :56-70 p=1, q=3 (sat_pos), idx[4] */
+#define MHE_MEAS_VEHICLE_PSEUDORANGE 3   /* :81-88 p=1, q=3               */
+#define MHE_MEAS_RANGE_3D 4              /* :39-54 p=1, q=3 ("y" form), idx[3] */
+
+typedef struct mhe_dims {
+  int32_t N;            /* collocation order; P = N + 1 CGL nodes            */
+  int32_t n;            /* state dimension   (must equal the model's)        */
+  int32_t m;            /* control dimension (must equal the model's)        */
+  int32_t p;            /* rows of one measurement (model's)                 */
+  int32_t M;            /* number of measurement times in the window         */
+  int32_t q;            /* per-row measurement parameters (0 if none)        */
+  int32_t dyn_model;    /* MHE_DYN_*                                         */
+  int32_t meas_model;   /* MHE_MEAS_*                                        */
+  int32_t has_prior;    /* 1: addInitialCost term present                    */
+  int32_t meas_idx[8];  /* static index params (params["idx"]), model-defined */
+  double T;             /* window length; node times tau2t(tau)              */
+} mhe_dims;
+
+/* Size in bytes of the device constants buffer for `dims` (0 on bad dims). */
+size_t mhe_const_bytes(const mhe_dims* dims);
+
+/*
+ * Build the per-problem device constants (one-time, NLP.build()).
+ *   D    (P,P)    negated CGL differentiation matrix   (collocation.py:42-64)
+ *   cw   (P)      (T/2) * w_k, w the reference weights   (nlp/nlp.py:245)
+ *   Phi  (M,P)    Lagrange basis at the measurement times (nlp/nlp.py:266)
+ *   Qw   (n,n)    dynamics-cost weight = params["Q"] of weighted_l2_norm
+ *   Rw   (M,p,p)  measurement information R passed to addResidualCost
+ *   Pw   (n,n)    prior weight (may be NULL when !has_prior)
+ * All six are DEVICE pointers; `const_buf` is a caller-owned device buffer of
+ * mhe_const_bytes(dims) bytes.
+ */
+int mhe_build_constants(const mhe_dims* dims, const double* D, const double* cw,
+                        const double* Phi, const double* Qw, const double* Rw,
+                        const double* Pw, void* const_buf, void* stream);
+
+/*
+ * Batched Gauss-Newton solve (NLP.solve()).  One trajectory per workgroup;
+ * the whole GN loop (residual + Jacobian, J^T W J / J^T W r assembly,
+ * Cholesky, triangular solves, update) runs inside one launch.
+ *   X0     (B,P,n)    initial iterate (warm start = previous solution)
+ *   X_out  (B,P,n)    solution (may alias X0)
+ *   U      (B|1,P,m)  controls at the nodes (setControl, nlp/nlp.py:304-308);
+ *                     NULL when m == 0
+ *   Y      (B,M,p)    measurements
+ *   PAR    (B|1,M,q)  per-row measurement params (sat_pos ...); NULL if q == 0
+ *   x0     (B,n)      prior mean (addInitialCost); NULL when !has_prior
+ *   cost_out (B) objective at X_out; iters_out (B) GN steps; status_out (B)
+ */
+int mhe_gn_solve(const mhe_dims* dims, const void* const_buf, int32_t batch,
+                 const double* X0, double* X_out,
+                 const double* U, int64_t u_bstride,
+                 const double* Y,
+                 const double* PAR, int64_t par_bstride,
+                 const double* x0,
+                 double* cost_out, int32_t* iters_out, int32_t* status_out,
+                 int32_t max_iter, double tol, void* stream);
+
+/* Padded system size used by the kernels: 16 * ceil(P*n / 16). */
+int32_t mhe_padded_dim(const mhe_dims* dims);
+
+/*
+ * Kernel-level parity: assemble the GN normal equations at X.
+ *   H (B,dp,dp) full symmetric (dp = mhe_padded_dim; padding rows = identity),
+ *   g (B,dp) gradient J^T W r (padding 0), cost (B).
+ */
+int mhe_assemble(const mhe_dims* dims, const void* const_buf, int32_t batch,
+                 const double* X, const double* U, int64_t u_bstride,
+                 const double* Y, const double* PAR, int64_t par_bstride,
+                 const double* x0, double* H, double* g, double* cost, void* stream);
+
+/*
+ * Kernel-level parity: solve H delta = -g for a batch of SPD matrices with the
+ * solver's register-tiled Cholesky.  H (B,dp,dp) (lower triangle read),
+ * g (B,dp), delta (B,dp), status (B).  `const_buf` is any constants buffer
+ * built for `dims` (only its tile table is read).
+ */
+int mhe_chol_solve(const mhe_dims* dims, const void* const_buf, int32_t batch,
+                   const double* H, const double* g, double* delta, int32_t* status,
+                   void* stream);
+
+/* Library version string. */
+const char* mhe_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MHE_H */

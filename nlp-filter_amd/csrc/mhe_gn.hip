@@ -1,0 +1,1058 @@
+// libmhe: batched collocation Gauss-Newton for MI355X (gfx950, CDNA4).
+//
+// What replaces what (reference kingdwd/nlp-filter):
+//   fixedTimeOptimalEstimationNLP objective   nlp/nlp.py:202-286
+//   NLP.solve() -> CasADi/IPOPT               nlp/nlp.py:61-83
+// is re-built here as ONE fused kernel per batch: one workgroup (4 waves) per
+// trajectory runs the whole Gauss-Newton loop
+//     residual + Jacobian  ->  J^T W J, J^T W r  ->  Cholesky  ->  2 triangular
+//     solves  ->  X += delta  ->  convergence test
+// with the d x d normal matrix (d = (N+1) n, padded to 16*NT) held in the MFMA
+// accumulator registers of the 4 waves as 16x16 fp64 tiles (lower triangle,
+// 2 KB per tile, 8 VGPRs per lane).  The right-looking blocked Cholesky
+// factors one 16-column panel per step in registers (row-per-lane sweep with
+// scalar broadcasts), streams the panel through LDS and applies the trailing
+// update with v_mfma_f64_16x16x4f64.  The forward solve rides along with the
+// panel sweep (augmented column); the backward solve reads L straight from the
+// tile registers.  Trajectories are independent: no inter-workgroup traffic.
+//
+// See DESIGN.md for the data layout, the roofline and the measurements.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "mhe.h"
+#include "mhe_models.h"
+
+namespace mhe {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+constexpr int NW = 4;              // waves per workgroup (one trajectory)
+constexpr int NTHREADS = NW * 64;
+constexpr int PBS = 18;            // panel-buffer row stride (doubles): 144 B, 16-B aligned,
+                                   // conflict-free for the MFMA operand reads
+constexpr int MAX_NT = 13;         // padded system <= 208 (register-resident path)
+constexpr int MAX_SLOTS = (MAX_NT * (MAX_NT + 1) / 2 + NW - 1) / NW;  // 23
+
+enum Mode { MODE_SOLVE = 0, MODE_ASSEMBLE = 1, MODE_LINSOLVE = 2 };
+
+// ------------------------------------------------------------ layouts
+struct ConstLayout {
+  size_t D, Dt, Phi, PhiT, cw, Qw, Pw, Rw, Cc, tab, total;  // byte offsets
+};
+
+__host__ __device__ inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+__host__ __device__ inline ConstLayout const_layout(int P, int M, int n, int p, int NT) {
+  ConstLayout L;
+  size_t o = 0;
+  const size_t ntiles = size_t(NT) * (NT + 1) / 2;
+  L.D = o;    o = align256(o + sizeof(double) * P * P);
+  L.Dt = o;   o = align256(o + sizeof(double) * P * P);
+  L.Phi = o;  o = align256(o + sizeof(double) * M * P);
+  L.PhiT = o; o = align256(o + sizeof(double) * M * P);
+  L.cw = o;   o = align256(o + sizeof(double) * P);
+  L.Qw = o;   o = align256(o + sizeof(double) * n * n);
+  L.Pw = o;   o = align256(o + sizeof(double) * n * n);
+  L.Rw = o;   o = align256(o + sizeof(double) * M * p * p);
+  L.Cc = o;   o = align256(o + sizeof(double) * ntiles * 256);
+  L.tab = o;  o = align256(o + sizeof(int) * ntiles);
+  L.total = o;
+  return L;
+}
+
+struct SmemLayout {  // offsets in doubles
+  int Xs, Vs, FtV, Es, FtE, GE, G, BV, DV, IDG, PB0, PB1, PART, RED, TAB, total;
+};
+
+__host__ __device__ inline int rnd2(int x) { return (x + 1) & ~1; }  // keep 16-B alignment
+
+__host__ __device__ inline SmemLayout smem_layout(int P, int M, int n, int NT, bool nonlinear) {
+  SmemLayout S;
+  int o = 0;
+  const int dp = 16 * NT;
+  S.Xs = o;   o += rnd2(P * n);
+  S.Vs = o;   o += rnd2(P * n);
+  S.FtV = o;  o += rnd2(P * n);
+  S.Es = o;   o += rnd2(P * n * n);
+  S.FtE = o;  o += rnd2(P * n * n);
+  S.GE = o;   o += rnd2(M * n);
+  S.G = o;    o += nonlinear ? rnd2(M * n * n) : 0;
+  S.BV = o;   o += dp;
+  S.DV = o;   o += dp;
+  S.IDG = o;  o += dp;
+  S.PB0 = o;  o += dp * PBS;
+  S.PB1 = o;  o += dp * PBS;
+  S.PART = o; o += NW * 16;
+  S.RED = o;  o += 4 * NW + 8;
+  S.TAB = o;  o += (NW * MAX_SLOTS + 1) / 2 + 1;  // int tile table (I | J << 16), -1 = no tile
+  S.total = o;
+  return S;
+}
+
+struct GnArgs {
+  const char* cbuf;
+  int P, M, d, NT, ntiles, q, has_prior;
+  int idx[8];
+  double alpha;
+  const double* X0;
+  double* Xout;
+  const double* U;
+  long long ustride;
+  const double* Y;
+  const double* PAR;
+  long long pstride;
+  const double* x0;
+  double* cost;
+  int* iters;
+  int* status;
+  int max_iter;
+  double tol;
+  double* Hout;
+  double* gout;
+  const double* Hin;
+  const double* gin;
+  double* dout;
+};
+
+// ------------------------------------------------------------ wave helpers
+__device__ __forceinline__ double readlane_d(double v, int lane) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)b, lane);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+  return v;
+}
+
+// block-wide reduction of up to 2 values (sum or max), result broadcast
+__device__ __forceinline__ void block_reduce2(double* red, double& a, double& b, bool is_max) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  a = is_max ? wave_max(a) : wave_sum(a);
+  b = is_max ? wave_max(b) : wave_sum(b);
+  if (lane == 0) {
+    red[2 * wave] = a;
+    red[2 * wave + 1] = b;
+  }
+  __syncthreads();
+  double ra = red[0], rb = red[1];
+#pragma unroll
+  for (int w = 1; w < NW; ++w) {
+    ra = is_max ? fmax(ra, red[2 * w]) : ra + red[2 * w];
+    rb = is_max ? fmax(rb, red[2 * w + 1]) : rb + red[2 * w + 1];
+  }
+  __syncthreads();
+  a = ra;
+  b = rb;
+}
+
+// Tile coordinates of linear tile t (column-major lower triangle), read from
+// the LDS copy of the table and made wave-uniform.  Reading from LDS (rather
+// than the constants buffer) keeps the compiler from hoisting 23 slots' worth
+// of table values out of the step loops into SGPRs.
+__device__ __forceinline__ int tile_IJ(const int* tab, int t) { return __builtin_amdgcn_readfirstlane(tab[t]); }
+
+// ------------------------------------------------------------ model phases
+// Per-node dynamics quantities (nlp/nlp.py:225-245):
+//   W_k = a * sum_j D_kj X_j - f(X_k, U_k);  V_k = c_k Qw W_k;  E_k = c_k Qw F_k;
+//   FtE_k = F_k^T E_k;  FtV_k = F_k^T V_k;   cost += c_k W_k^T Qw W_k
+template <class DYN>
+__device__ __forceinline__ double node_phase(const GnArgs& a, const ConstLayout& CL, const SmemLayout& SL, double* sm, int b) {
+  constexpr int n = DYN::n, m = DYN::m;
+  const double* Dt = (const double*)(a.cbuf + CL.Dt);
+  const double* cw = (const double*)(a.cbuf + CL.cw);
+  const double* Qw = (const double*)(a.cbuf + CL.Qw);
+  const double* Xs = sm + SL.Xs;
+  double cost = 0.0;
+  for (int k = threadIdx.x; k < a.P; k += NTHREADS) {
+    double dx[n];
+#pragma unroll
+    for (int c = 0; c < n; ++c) dx[c] = 0.0;
+    for (int j = 0; j < a.P; ++j) {
+      const double djk = Dt[j * a.P + k];
+#pragma unroll
+      for (int c = 0; c < n; ++c) dx[c] += djk * Xs[j * n + c];
+    }
+    double xk[n], uk[m > 0 ? m : 1], f[n], F[n * n];
+#pragma unroll
+    for (int c = 0; c < n; ++c) xk[c] = Xs[k * n + c];
+    if (m > 0) {
+      const double* U = a.U + (long long)b * a.ustride + (long long)k * m;
+#pragma unroll
+      for (int c = 0; c < m; ++c) uk[c] = U[c];
+    }
+    DYN::eval(xk, uk, f, F);
+    double W[n], V[n];
+#pragma unroll
+    for (int c = 0; c < n; ++c) W[c] = a.alpha * dx[c] - f[c];
+    const double ck = cw[k];
+#pragma unroll
+    for (int r = 0; r < n; ++r) {
+      double s = 0.0;
+#pragma unroll
+      for (int c = 0; c < n; ++c) s += Qw[r * n + c] * W[c];
+      V[r] = ck * s;
+      cost += W[r] * V[r];
+    }
+    double E[n * n];
+#pragma unroll
+    for (int r = 0; r < n; ++r)
+#pragma unroll
+      for (int c = 0; c < n; ++c) {
+        double s = 0.0;
+#pragma unroll
+        for (int t = 0; t < n; ++t) s += Qw[r * n + t] * F[t * n + c];
+        E[r * n + c] = ck * s;
+      }
+    double* Vs = sm + SL.Vs + k * n;
+    double* FtV = sm + SL.FtV + k * n;
+    double* Es = sm + SL.Es + k * n * n;
+    double* FtE = sm + SL.FtE + k * n * n;
+#pragma unroll
+    for (int r = 0; r < n; ++r) {
+      Vs[r] = V[r];
+      double s = 0.0;
+#pragma unroll
+      for (int t = 0; t < n; ++t) s += F[t * n + r] * V[t];
+      FtV[r] = s;
+#pragma unroll
+      for (int c = 0; c < n; ++c) {
+        Es[r * n + c] = E[r * n + c];
+        double u = 0.0;
+#pragma unroll
+        for (int t = 0; t < n; ++t) u += F[t * n + r] * E[t * n + c];
+        FtE[r * n + c] = u;
+      }
+    }
+  }
+  return cost;
+}
+
+// Per-measurement-row quantities (nlp/nlp.py:264-273):
+//   x_i = sum_j Phi_ij X_j;  e_i = y_i - h(x_i);  GE_i = H_i^T Rw_i e_i;
+//   (nonlinear) G_i = H_i^T Rw_i H_i;  cost += e_i^T Rw_i e_i
+template <class DYN, class MEAS>
+__device__ __forceinline__ double meas_phase(const GnArgs& a, const ConstLayout& CL, const SmemLayout& SL, double* sm, int b) {
+  constexpr int n = DYN::n, p = MEAS::p, q = MEAS::q;
+  const double* PhiT = (const double*)(a.cbuf + CL.PhiT);
+  const double* Rw = (const double*)(a.cbuf + CL.Rw);
+  const double* Xs = sm + SL.Xs;
+  double cost = 0.0;
+  for (int i = threadIdx.x; i < a.M; i += NTHREADS) {
+    double xi[n];
+#pragma unroll
+    for (int c = 0; c < n; ++c) xi[c] = 0.0;
+    for (int j = 0; j < a.P; ++j) {
+      const double ph = PhiT[j * a.M + i];
+#pragma unroll
+      for (int c = 0; c < n; ++c) xi[c] += ph * Xs[j * n + c];
+    }
+    double par[q > 0 ? q : 1];
+    if (q > 0) {
+      const double* PR = a.PAR + (long long)b * a.pstride + (long long)i * q;
+#pragma unroll
+      for (int c = 0; c < q; ++c) par[c] = PR[c];
+    }
+    double h[p], H[p * n];
+    MEAS::eval(xi, par, a.idx, h, H);
+    const double* yi = a.Y + ((long long)b * a.M + i) * p;
+    const double* R = Rw + (long long)i * p * p;
+    double e[p], Re[p];
+#pragma unroll
+    for (int r = 0; r < p; ++r) e[r] = yi[r] - h[r];
+#pragma unroll
+    for (int r = 0; r < p; ++r) {
+      double s = 0.0;
+#pragma unroll
+      for (int c = 0; c < p; ++c) s += R[r * p + c] * e[c];
+      Re[r] = s;
+      cost += e[r] * s;
+    }
+    double* GE = sm + SL.GE + i * n;
+#pragma unroll
+    for (int c = 0; c < n; ++c) {
+      double s = 0.0;
+#pragma unroll
+      for (int r = 0; r < p; ++r) s += H[r * n + c] * Re[r];
+      GE[c] = s;
+    }
+    if (!MEAS::LINEAR) {
+      double* G = sm + SL.G + i * n * n;
+      double RH[p * n];
+#pragma unroll
+      for (int r = 0; r < p; ++r)
+#pragma unroll
+        for (int c = 0; c < n; ++c) {
+          double s = 0.0;
+#pragma unroll
+          for (int t = 0; t < p; ++t) s += R[r * p + t] * H[t * n + c];
+          RH[r * n + c] = s;
+        }
+#pragma unroll
+      for (int r = 0; r < n; ++r)
+#pragma unroll
+        for (int c = 0; c < n; ++c) {
+          double s = 0.0;
+#pragma unroll
+          for (int t = 0; t < p; ++t) s += H[t * n + r] * RH[t * n + c];
+          G[r * n + c] = s;
+        }
+    }
+  }
+  return cost;
+}
+
+// Gradient g = J^T W r; writes BV = -g (padding 0).  Also the prior cost.
+template <class DYN>
+__device__ __forceinline__ double grad_phase(const GnArgs& a, const ConstLayout& CL, const SmemLayout& SL, double* sm, int b) {
+  constexpr int n = DYN::n;
+  const double* D = (const double*)(a.cbuf + CL.D);
+  const double* Phi = (const double*)(a.cbuf + CL.Phi);
+  const double* Pw = (const double*)(a.cbuf + CL.Pw);
+  const double* Vs = sm + SL.Vs;
+  const double* FtV = sm + SL.FtV;
+  const double* GE = sm + SL.GE;
+  const double* Xs = sm + SL.Xs;
+  double* BV = sm + SL.BV;
+  double cost = 0.0;
+  const int dp = 16 * a.NT;
+  for (int j = threadIdx.x; j < a.P; j += NTHREADS) {
+    double gv[n];
+#pragma unroll
+    for (int c = 0; c < n; ++c) gv[c] = 0.0;
+    for (int k = 0; k < a.P; ++k) {
+      const double dkj = D[k * a.P + j];
+#pragma unroll
+      for (int c = 0; c < n; ++c) gv[c] += dkj * Vs[k * n + c];
+    }
+#pragma unroll
+    for (int c = 0; c < n; ++c) gv[c] = a.alpha * gv[c] - FtV[j * n + c];
+    for (int i = 0; i < a.M; ++i) {
+      const double ph = Phi[i * a.P + j];
+#pragma unroll
+      for (int c = 0; c < n; ++c) gv[c] -= ph * GE[i * n + c];
+    }
+    if (a.has_prior && j == 0) {
+      double r0[n];
+#pragma unroll
+      for (int c = 0; c < n; ++c) r0[c] = Xs[c] - a.x0[(long long)b * n + c];
+#pragma unroll
+      for (int r = 0; r < n; ++r) {
+        double s = 0.0;
+#pragma unroll
+        for (int c = 0; c < n; ++c) s += Pw[r * n + c] * r0[c];
+        gv[r] += s;
+        cost += r0[r] * s;
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < n; ++c) BV[j * n + c] = -gv[c];
+  }
+  for (int t = a.d + threadIdx.x; t < dp; t += NTHREADS) BV[t] = 0.0;
+  return cost;
+}
+
+// Build the H tiles owned by this wave:
+//   H = Cc (constant: a^2 (D^T C D) (x) Qw  + linear-measurement term + prior + padding I)
+//     - a D_lj E_l[a,b] - a D_jl E_j[b,a] + delta_jl (F^T E)_j[a,b]      (dynamics, X-dependent)
+//     + sum_i Phi_ij Phi_il G_i[a,b]                                      (nonlinear measurements)
+template <class DYN, class MEAS, int SLOTS>
+__device__ __forceinline__ void build_tiles(const GnArgs& a, const ConstLayout& CL, const SmemLayout& SL, double* sm,
+                            d4 (&acc)[SLOTS], int wave, int lane) {
+  constexpr int n = DYN::n;
+  const double* Cc = (const double*)(a.cbuf + CL.Cc);
+  const double* D = (const double*)(a.cbuf + CL.D);
+  const double* Phi = (const double*)(a.cbuf + CL.Phi);
+  const int* tab = (const int*)(sm + SL.TAB);
+  const double* Es = sm + SL.Es;
+  const double* FtE = sm + SL.FtE;
+  const double* G = sm + SL.G;
+  // opaque copies: the per-slot tile pointers would otherwise be hoisted out
+  // of the Gauss-Newton loop (23 live 64-bit addresses -> spills)
+  asm volatile("" : "+v"(lane));
+  asm volatile("" : "+s"(wave));
+#pragma unroll
+  for (int s = 0; s < SLOTS; ++s) {
+    const int t = wave + NW * s;
+    const int IJ = tile_IJ(tab, t);
+    if (IJ < 0) {
+      acc[s] = d4{0.0, 0.0, 0.0, 0.0};  // no tile: always define (keeps acc dead between iterations)
+    } else {
+      const int I = IJ & 0xffff, J = IJ >> 16;
+      const double* ct = Cc + (size_t)t * 256 + lane;
+      const int col = 16 * J + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        double v = ct[64 * r];
+        const int row = 16 * I + (lane >> 4) + 4 * r;
+        if (row < a.d && col < a.d) {
+          const int j = row / n, aa = row - j * n;
+          const int l = col / n, bb = col - l * n;
+          v -= a.alpha * (D[l * a.P + j] * Es[(l * n + aa) * n + bb] + D[j * a.P + l] * Es[(j * n + bb) * n + aa]);
+          if (j == l) v += FtE[(j * n + aa) * n + bb];
+          if (!MEAS::LINEAR) {
+            double s2 = 0.0;
+            for (int i = 0; i < a.M; ++i) s2 += Phi[i * a.P + j] * Phi[i * a.P + l] * G[(i * n + aa) * n + bb];
+            v += s2;
+          }
+        }
+        acc[s][r] = v;
+      }
+    }
+  }
+}
+
+// Load H tiles from a dense (dp x dp) matrix (MODE_LINSOLVE).
+template <int SLOTS>
+__device__ __forceinline__ void load_tiles(const GnArgs& a, const int* tab, const double* Hb, d4 (&acc)[SLOTS], int wave, int lane) {
+  // tab: LDS table with -1 sentinels
+  const int dp = 16 * a.NT;
+#pragma unroll
+  for (int s = 0; s < SLOTS; ++s) {
+    const int t = wave + NW * s;
+    const int IJ = tile_IJ(tab, t);
+    if (IJ < 0) {
+      acc[s] = d4{0.0, 0.0, 0.0, 0.0};
+    } else {
+      const int I = IJ & 0xffff, J = IJ >> 16;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * I + (lane >> 4) + 4 * r, col = 16 * J + (lane & 15);
+        acc[s][r] = Hb[(size_t)row * dp + col];
+      }
+    }
+  }
+}
+
+// Right-looking blocked Cholesky H = L L^T with the forward solve L y = BV
+// fused (BV <- y).  L stays in the tile registers.  Returns false if a pivot
+// was not positive/finite.
+template <int SLOTS>
+__device__ __forceinline__ bool factor_forward(const GnArgs& a, const int* tab, const SmemLayout& SL, double* sm,
+                                               d4 (&acc)[SLOTS], int wave, int lane) {
+  double* BV = sm + SL.BV;
+  double* IDG = sm + SL.IDG;
+  int* flag = (int*)(sm + SL.RED + 4 * NW);
+  if (threadIdx.x == 0) flag[0] = 0;
+  const int NT = a.NT;
+  // lane-dependent LDS offsets shared by every slot
+  const int c_off = ((lane >> 4) * PBS + (lane & 15));   // C-layout element (row g, col c)
+  const int ab_off = ((lane & 15) * PBS + (lane >> 4));  // MFMA A/B operand (row l&15, k l>>4)
+#pragma unroll 1
+  for (int k = 0; k < NT; ++k) {
+    // opaque per-step copies: keep LICM from hoisting 23 slot predicates and
+    // 16 lane masks out of the step loop (they would spill SGPRs)
+    int lane_o = lane, wave_o = wave;
+    asm volatile("" : "+v"(lane_o));
+    asm volatile("" : "+s"(wave_o));
+    double* PB = sm + ((k & 1) ? SL.PB1 : SL.PB0);
+    // (1) panel k -> LDS
+#pragma unroll
+    for (int s = 0; s < SLOTS; ++s) {
+      const int t = wave_o + NW * s;
+      {
+        const int IJ = tile_IJ(tab, t);
+        const int I = IJ & 0xffff, J = IJ >> 16;
+        if (J == k) {
+          double* dst = PB + (I - k) * 16 * PBS + c_off;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) dst[4 * r * PBS] = acc[s][r];
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __syncthreads();
+    // (2) panel sweep: row per lane; every wave redundantly holds the 16
+    //     diagonal-block rows in lanes 0..15, lanes 16..63 take 48 panel rows each.
+    {
+      const int prow = (lane_o < 16) ? lane : 16 + wave_o * 48 + (lane_o - 16);
+      const bool valid = prow < 16 * (NT - k);
+      const bool mine = (lane_o < 16) ? (wave_o == 0) : valid;
+      // lanes past the panel read row 0 (finite data) and never write back
+      const int lrow = valid ? prow : 0;
+      double r[16];
+      const double* src = PB + lrow * PBS;
+#pragma unroll
+      for (int c = 0; c < 16; c += 2) {
+        const double2 v = *(const double2*)(src + c);
+        r[c] = v.x;
+        r[c + 1] = v.y;
+      }
+      double bb = BV[16 * k + lrow];
+      double myrs = 0.0;
+      bool bad = false;
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        double piv = readlane_d(r[c], c);
+        if (!(piv > 0.0) || !isfinite(piv)) {
+          bad = true;
+          piv = 1.0;
+        }
+        const double rs = rsqrt(piv);
+        const double sq = piv * rs;
+        r[c] = (lane_o == c) ? sq : r[c] * rs;
+        const double yc = readlane_d(bb, c) * rs;
+        if (lane_o == c) {
+          myrs = rs;
+          bb = yc;
+        } else if (lane_o > c) {
+          bb -= r[c] * yc;
+        }
+#pragma unroll
+        for (int s2 = c + 1; s2 < 16; ++s2) {
+          const double Lsc = readlane_d(r[c], s2);
+          r[s2] -= r[c] * Lsc;
+        }
+      }
+      if (mine) {
+        double* dst = PB + prow * PBS;
+#pragma unroll
+        for (int c = 0; c < 16; c += 2) *(double2*)(dst + c) = make_double2(r[c], r[c + 1]);
+        BV[16 * k + prow] = bb;
+        if (lane_o < 16) IDG[16 * k + lane] = myrs;
+      }
+      if (bad && wave_o == 0 && lane_o == 0) flag[0] = 1;
+    }
+    __syncthreads();
+    // (3) reload the factored panel into its tiles; trailing update with MFMA
+#pragma unroll
+    for (int s = 0; s < SLOTS; ++s) {
+      const int t = wave_o + NW * s;
+      {
+        const int IJ = tile_IJ(tab, t);
+        const int I = IJ & 0xffff, J = IJ >> 16;
+        if (J == k) {
+          const double* srcp = PB + (I - k) * 16 * PBS + c_off;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int tr = (lane >> 4) + 4 * r, tc = lane & 15;
+            const double v = srcp[4 * r * PBS];
+            acc[s][r] = (I == k && tr < tc) ? 0.0 : v;
+          }
+        } else if (J > k) {
+          const double* ai = PB + (I - k) * 16 * PBS + ab_off;
+          const double* bj = PB + (J - k) * 16 * PBS + ab_off;
+          double av[4], bv[4];
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq) {
+            av[qq] = ai[4 * qq];
+            bv[qq] = bj[4 * qq];
+          }
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq)
+            acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(-av[qq], bv[qq], acc[s], 0, 0, 0);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  __syncthreads();
+  return flag[0] == 0;
+}
+
+// Backward solve L^T delta = y (y in BV) -> DV.
+template <int SLOTS>
+__device__ __forceinline__ void backward(const GnArgs& a, const int* tab, const SmemLayout& SL, double* sm,
+                                         d4 (&acc)[SLOTS], int wave, int lane) {
+  const double* BV = sm + SL.BV;
+  const double* IDG = sm + SL.IDG;
+  double* DV = sm + SL.DV;
+  double* PART = sm + SL.PART;
+  double* LK = sm + SL.PB0;  // 16 x PBS scratch
+  const int NT = a.NT;
+  const int c_off = ((lane >> 4) * PBS + (lane & 15));
+#pragma unroll 1
+  for (int k = NT - 1; k >= 0; --k) {
+    int lane_o = lane, wave_o = wave;
+    asm volatile("" : "+v"(lane_o));
+    asm volatile("" : "+s"(wave_o));
+    double pv = 0.0;
+#pragma unroll
+    for (int s = 0; s < SLOTS; ++s) {
+      const int t = wave_o + NW * s;
+      {
+        const int IJ = tile_IJ(tab, t);
+        const int I = IJ & 0xffff, J = IJ >> 16;
+        if (J == k) {
+          if (I > k) {
+            const double* dv = DV + 16 * I + (lane >> 4);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) pv += acc[s][r] * dv[4 * r];
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) LK[c_off + 4 * r * PBS] = acc[s][r];
+          }
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    pv += __shfl_xor(pv, 16);
+    pv += __shfl_xor(pv, 32);
+    if (lane < 16) PART[wave * 16 + lane] = pv;
+    __syncthreads();
+    if (wave_o == 0 && lane_o < 16) {
+      double rhs = BV[16 * k + lane_o];
+#pragma unroll
+      for (int w = 0; w < NW; ++w) rhs -= PART[w * 16 + lane_o];
+      const double idg = IDG[16 * k + lane_o];
+#pragma unroll
+      for (int s2 = 15; s2 >= 0; --s2) {
+        const double ds = readlane_d(rhs, s2) * readlane_d(idg, s2);
+        if (lane_o == s2) rhs = ds;
+        else if (lane_o < s2) rhs -= LK[s2 * PBS + lane_o] * ds;
+      }
+      DV[16 * k + lane_o] = rhs;
+    }
+    __syncthreads();
+  }
+}
+
+template <class DYN, class MEAS, int SLOTS, int mode>
+__global__ __launch_bounds__(NTHREADS, 2) void k_gn(GnArgs a) {
+  constexpr int n = DYN::n;
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  const ConstLayout CL = const_layout(a.P, a.M, n, MEAS::p, a.NT);
+  const SmemLayout SL = smem_layout(a.P, a.M, n, a.NT, !MEAS::LINEAR);
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int b = blockIdx.x;
+  int* tab = (int*)(sm + SL.TAB);
+  {
+    const int* gtab = (const int*)(a.cbuf + CL.tab);
+    for (int t = threadIdx.x; t < NW * MAX_SLOTS; t += NTHREADS) tab[t] = (t < a.ntiles) ? gtab[t] : -1;
+  }
+  double* Xs = sm + SL.Xs;
+  double* DV = sm + SL.DV;
+  double* RED = sm + SL.RED;
+  d4 acc[SLOTS];
+#pragma unroll
+  for (int s = 0; s < SLOTS; ++s) acc[s] = d4{0.0, 0.0, 0.0, 0.0};
+
+  __syncthreads();
+  if constexpr (mode == MODE_LINSOLVE) {
+    const int dp = 16 * a.NT;
+    const double* Hb = a.Hin + (size_t)b * dp * dp;
+    for (int t = threadIdx.x; t < dp; t += NTHREADS) sm[SL.BV + t] = -a.gin[(size_t)b * dp + t];
+    load_tiles<SLOTS>(a, tab, Hb, acc, wave, lane);
+    __syncthreads();
+    const bool ok = factor_forward<SLOTS>(a, tab, SL, sm, acc, wave, lane);
+    backward<SLOTS>(a, tab, SL, sm, acc, wave, lane);
+    for (int t = threadIdx.x; t < dp; t += NTHREADS) a.dout[(size_t)b * dp + t] = DV[t];
+    if (threadIdx.x == 0) a.status[b] = ok ? MHE_STATUS_CONVERGED : MHE_STATUS_NOT_SPD;
+    return;
+  }
+
+  for (int t = threadIdx.x; t < a.d; t += NTHREADS) Xs[t] = a.X0[(size_t)b * a.d + t];
+  __syncthreads();
+
+  int status = MHE_STATUS_MAX_ITER;
+  int it = 0;
+  for (;;) {
+    double c1 = node_phase<DYN>(a, CL, SL, sm, b);
+    c1 += meas_phase<DYN, MEAS>(a, CL, SL, sm, b);
+    __syncthreads();
+    c1 += grad_phase<DYN>(a, CL, SL, sm, b);
+    if constexpr (mode == MODE_ASSEMBLE) {
+      double c2 = 0.0;
+      block_reduce2(RED, c1, c2, false);
+      build_tiles<DYN, MEAS, SLOTS>(a, CL, SL, sm, acc, wave, lane);
+      const int dp = 16 * a.NT;
+      double* Hb = a.Hout + (size_t)b * dp * dp;
+#pragma unroll
+      for (int s = 0; s < SLOTS; ++s) {
+        const int t = wave + NW * s;
+        if (t < a.ntiles) {
+          const int IJ = tile_IJ(tab, t);
+          const int I = IJ & 0xffff, J = IJ >> 16;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = 16 * I + (lane >> 4) + 4 * r, col = 16 * J + (lane & 15);
+            Hb[(size_t)row * dp + col] = acc[s][r];
+            if (I != J) Hb[(size_t)col * dp + row] = acc[s][r];
+          }
+        }
+      }
+      for (int t = threadIdx.x; t < dp; t += NTHREADS) a.gout[(size_t)b * dp + t] = -sm[SL.BV + t];
+      if (threadIdx.x == 0) a.cost[b] = c1;
+      return;
+    }
+    if (it >= a.max_iter) break;
+    build_tiles<DYN, MEAS, SLOTS>(a, CL, SL, sm, acc, wave, lane);
+    __syncthreads();
+    const bool ok = factor_forward<SLOTS>(a, tab, SL, sm, acc, wave, lane);
+    if (!ok) {
+      status = MHE_STATUS_NOT_SPD;
+      break;
+    }
+    backward<SLOTS>(a, tab, SL, sm, acc, wave, lane);
+    double dmax = 0.0, xmax = 0.0;
+    bool finite = true;
+    for (int t = threadIdx.x; t < a.d; t += NTHREADS) {
+      const double dv = DV[t];
+      finite = finite && isfinite(dv);
+      dmax = fmax(dmax, fabs(dv));
+    }
+    double fin = finite ? 0.0 : 1.0;
+    block_reduce2(RED, dmax, fin, true);
+    if (fin != 0.0) {
+      status = MHE_STATUS_NONFINITE;
+      break;
+    }
+    for (int t = threadIdx.x; t < a.d; t += NTHREADS) {
+      const double xv = Xs[t] + DV[t];
+      Xs[t] = xv;
+      xmax = fmax(xmax, fabs(xv));
+    }
+    double dummy = 0.0;
+    block_reduce2(RED, xmax, dummy, true);
+    ++it;
+    if (dmax <= a.tol * (1.0 + xmax)) {
+      status = MHE_STATUS_CONVERGED;
+      // final cost at the converged iterate
+      double cf = node_phase<DYN>(a, CL, SL, sm, b);
+      cf += meas_phase<DYN, MEAS>(a, CL, SL, sm, b);
+      __syncthreads();
+      cf += grad_phase<DYN>(a, CL, SL, sm, b);
+      double z = 0.0;
+      block_reduce2(RED, cf, z, false);
+      if (threadIdx.x == 0) a.cost[b] = cf;
+      goto done;
+    }
+  }
+  {
+    // cost at the returned iterate (the loop's last residual pass is at Xs
+    // unless the iteration broke before updating)
+    double cf = node_phase<DYN>(a, CL, SL, sm, b);
+    cf += meas_phase<DYN, MEAS>(a, CL, SL, sm, b);
+    __syncthreads();
+    cf += grad_phase<DYN>(a, CL, SL, sm, b);
+    double z = 0.0;
+    block_reduce2(RED, cf, z, false);
+    if (threadIdx.x == 0) a.cost[b] = cf;
+  }
+done:
+  __syncthreads();
+  for (int t = threadIdx.x; t < a.d; t += NTHREADS) a.Xout[(size_t)b * a.d + t] = Xs[t];
+  if (threadIdx.x == 0) {
+    a.iters[b] = it;
+    a.status[b] = status;
+  }
+}
+
+// ------------------------------------------------------------ constants
+// Cc tile element (row, col) of the constant part of J^T W J.
+template <class MEAS>
+__global__ void k_build_cc(int P, int M, int n, int p, int NT, int has_prior, double alpha,
+                           const double* D, const double* cw, const double* Phi, const double* Qw,
+                           const double* Rw, const double* Pw, char* cbuf) {
+  const ConstLayout CL = const_layout(P, M, n, p, NT);
+  const int ntiles = NT * (NT + 1) / 2;
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= ntiles * 256) return;
+  const int t = gid >> 8, e = gid & 255, r = e >> 6, lane = e & 63;
+  // tile t -> (I, J): column-major over the lower triangle
+  int J = 0, base = 0;
+  while (t >= base + (NT - J)) {
+    base += NT - J;
+    ++J;
+  }
+  const int I = J + (t - base);
+  const int row = 16 * I + (lane >> 4) + 4 * r, col = 16 * J + (lane & 15);
+  const int d = P * n;
+  double v;
+  if (row < d && col < d) {
+    const int j = row / n, a = row % n, l = col / n, bb = col % n;
+    double dcd = 0.0;
+    for (int k = 0; k < P; ++k) dcd += D[k * P + j] * cw[k] * D[k * P + l];
+    v = alpha * alpha * dcd * Qw[a * n + bb];
+    if (MEAS::LINEAR) {  // full_state: H_i = I, G_i = Rw_i
+      double s = 0.0;
+      for (int i = 0; i < M; ++i) s += Phi[i * P + j] * Phi[i * P + l] * Rw[(i * p + a) * p + bb];
+      v += s;
+    }
+    if (has_prior && j == 0 && l == 0) v += Pw[a * n + bb];
+  } else {
+    v = (row == col) ? 1.0 : 0.0;
+  }
+  double* Cc = (double*)(cbuf + CL.Cc);
+  Cc[(size_t)t * 256 + r * 64 + lane] = v;
+  if (e == 0) {
+    int* tab = (int*)(cbuf + CL.tab);
+    tab[t] = I | (J << 16);
+  }
+}
+
+__global__ void k_copy_consts(int P, int M, int n, int p, int NT, const double* D, const double* cw,
+                              const double* Phi, const double* Qw, const double* Rw, const double* Pw,
+                              char* cbuf) {
+  const ConstLayout CL = const_layout(P, M, n, p, NT);
+  double* oD = (double*)(cbuf + CL.D);
+  double* oDt = (double*)(cbuf + CL.Dt);
+  double* oPhi = (double*)(cbuf + CL.Phi);
+  double* oPhiT = (double*)(cbuf + CL.PhiT);
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int stride = gridDim.x * blockDim.x;
+  for (int e = gid; e < P * P; e += stride) {
+    const int k = e / P, j = e % P;
+    oD[e] = D[e];
+    oDt[j * P + k] = D[e];
+  }
+  for (int e = gid; e < M * P; e += stride) {
+    const int i = e / P, j = e % P;
+    oPhi[e] = Phi[e];
+    oPhiT[j * M + i] = Phi[e];
+  }
+  for (int e = gid; e < P; e += stride) ((double*)(cbuf + CL.cw))[e] = cw[e];
+  for (int e = gid; e < n * n; e += stride) {
+    ((double*)(cbuf + CL.Qw))[e] = Qw[e];
+    ((double*)(cbuf + CL.Pw))[e] = Pw ? Pw[e] : 0.0;
+  }
+  for (int e = gid; e < M * p * p; e += stride) ((double*)(cbuf + CL.Rw))[e] = Rw[e];
+}
+
+}  // namespace mhe
+
+// ================================================================ dispatch
+using namespace mhe;
+
+namespace {
+
+struct ModelInfo {
+  int n, m, p, q;
+  bool linear;
+};
+
+bool dyn_info(int id, int& n, int& m) {
+  switch (id) {
+    case MHE_DYN_SINGLE_INTEGRATOR: n = 1; m = 1; return true;
+    case MHE_DYN_SINGLE_INTEGRATOR_2D: n = 2; m = 2; return true;
+    case MHE_DYN_SINGLE_INTEGRATOR_3D: n = 3; m = 3; return true;
+    case MHE_DYN_DOUBLE_INTEGRATOR: n = 4; m = 2; return true;
+    case MHE_DYN_VAN_DER_POL: n = 2; m = 1; return true;
+    case MHE_DYN_GNSS_POS_AND_BIAS: n = 5; m = 3; return true;
+    case MHE_DYN_MULTI_RECEIVER: n = 8; m = 0; return true;
+    case MHE_DYN_GNSS_TWO_RECEIVER: n = 10; m = 6; return true;
+    case MHE_DYN_KINEMATIC_BICYCLE: n = 6; m = 2; return true;
+  }
+  return false;
+}
+
+bool meas_info(int id, int n, int& p, int& q, bool& linear) {
+  switch (id) {
+    case MHE_MEAS_FULL_STATE: p = n; q = 0; linear = true; return true;
+    case MHE_MEAS_PSEUDORANGE: p = 1; q = 3; linear = false; return true;
+    case MHE_MEAS_VEHICLE_PSEUDORANGE: p = 1; q = 3; linear = false; return true;
+    case MHE_MEAS_RANGE_3D: p = 1; q = 3; linear = false; return true;
+  }
+  return false;
+}
+
+int check_dims(const mhe_dims* dm, int* NT_out) {
+  if (!dm) return MHE_ERR_NULL;
+  int n, m, p, q;
+  bool lin;
+  if (!dyn_info(dm->dyn_model, n, m)) return MHE_ERR_MODEL;
+  if (!meas_info(dm->meas_model, n, p, q, lin)) return MHE_ERR_MODEL;
+  if (dm->n != n || dm->m != m || dm->p != p || dm->q != q) return MHE_ERR_DIMS;
+  if (dm->N < 1 || dm->M < 0 || !(dm->T > 0.0)) return MHE_ERR_DIMS;
+  if (dm->meas_model == MHE_MEAS_VEHICLE_PSEUDORANGE && n < 9) return MHE_ERR_DIMS;
+  for (int i = 0; i < 4; ++i)
+    if ((dm->meas_model == MHE_MEAS_PSEUDORANGE && (dm->meas_idx[i] < 0 || dm->meas_idx[i] >= n)) ||
+        (dm->meas_model == MHE_MEAS_RANGE_3D && i < 3 && (dm->meas_idx[i] < 0 || dm->meas_idx[i] >= n)))
+      return MHE_ERR_DIMS;
+  const int P = dm->N + 1;
+  const int NT = (P * n + 15) / 16;
+  if (NT > MAX_NT) return MHE_ERR_UNSUPPORTED;
+  if (NT_out) *NT_out = NT;
+  return MHE_OK;
+}
+
+int smem_bytes(const mhe_dims* dm, int NT) {
+  int p, q;
+  bool lin;
+  meas_info(dm->meas_model, dm->n, p, q, lin);
+  return smem_layout(dm->N + 1, dm->M, dm->n, NT, !lin).total * (int)sizeof(double);
+}
+
+template <class DYN, class MEAS>
+int launch_gn(const mhe_dims* dm, GnArgs& a, int batch, int mode, hipStream_t st) {
+  const int smem = smem_bytes(dm, a.NT);
+  if (smem > 160 * 1024) return MHE_ERR_UNSUPPORTED;
+  void (*kern)(GnArgs) = nullptr;
+  if (mode == MODE_SOLVE) kern = k_gn<DYN, MEAS, MAX_SLOTS, MODE_SOLVE>;
+  else if (mode == MODE_ASSEMBLE) kern = k_gn<DYN, MEAS, MAX_SLOTS, MODE_ASSEMBLE>;
+  else kern = k_gn<DYN, MEAS, MAX_SLOTS, MODE_LINSOLVE>;
+  if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem) != hipSuccess)
+    return MHE_ERR_HIP;
+  hipLaunchKernelGGL(kern, dim3(batch), dim3(NTHREADS), smem, st, a);
+  return hipGetLastError() == hipSuccess ? MHE_OK : MHE_ERR_HIP;
+}
+
+template <class MEAS>
+int launch_cc(const mhe_dims* dm, int NT, const double* D, const double* cw, const double* Phi,
+              const double* Qw, const double* Rw, const double* Pw, char* cbuf, hipStream_t st) {
+  const int P = dm->N + 1;
+  const int ntiles = NT * (NT + 1) / 2;
+  hipLaunchKernelGGL(k_copy_consts, dim3(256), dim3(256), 0, st, P, dm->M, dm->n, dm->p, NT, D, cw, Phi, Qw,
+                     Rw, Pw, cbuf);
+  hipLaunchKernelGGL(k_build_cc<MEAS>, dim3((ntiles * 256 + 255) / 256), dim3(256), 0, st, P, dm->M, dm->n,
+                     dm->p, NT, dm->has_prior, 2.0 / dm->T, D, cw, Phi, Qw, Rw, Pw, cbuf);
+  return hipGetLastError() == hipSuccess ? MHE_OK : MHE_ERR_HIP;
+}
+
+// model dispatch: calls F.template operator()<DYN, MEAS>()
+template <class F>
+int dispatch(const mhe_dims* dm, F&& f) {
+  switch (dm->dyn_model) {
+    case MHE_DYN_VAN_DER_POL:
+      if (dm->meas_model == MHE_MEAS_FULL_STATE) return f.template run<DynVanDerPol, MeasFullState<2>>();
+      break;
+#ifndef MHE_FAST_BUILD  // -DMHE_FAST_BUILD: van der Pol only (kernel development)
+    case MHE_DYN_SINGLE_INTEGRATOR:
+      if (dm->meas_model == MHE_MEAS_FULL_STATE) return f.template run<DynSingleIntegrator, MeasFullState<1>>();
+      break;
+    case MHE_DYN_SINGLE_INTEGRATOR_2D:
+      if (dm->meas_model == MHE_MEAS_FULL_STATE) return f.template run<DynSingleIntegratorND<2>, MeasFullState<2>>();
+      break;
+    case MHE_DYN_GNSS_POS_AND_BIAS:
+      if (dm->meas_model == MHE_MEAS_PSEUDORANGE) return f.template run<DynGnssPosAndBias, MeasPseudorange<5>>();
+      if (dm->meas_model == MHE_MEAS_FULL_STATE) return f.template run<DynGnssPosAndBias, MeasFullState<5>>();
+      break;
+    case MHE_DYN_KINEMATIC_BICYCLE:
+      if (dm->meas_model == MHE_MEAS_PSEUDORANGE) return f.template run<DynKinematicBicycle, MeasPseudorange<6>>();
+      break;
+    case MHE_DYN_DOUBLE_INTEGRATOR:
+      if (dm->meas_model == MHE_MEAS_FULL_STATE) return f.template run<DynDoubleIntegrator, MeasFullState<4>>();
+      break;
+#endif
+    default:
+      break;
+  }
+  return MHE_ERR_UNSUPPORTED;
+}
+
+GnArgs make_args(const mhe_dims* dm, const void* cbuf, int NT) {
+  GnArgs a = {};
+  a.cbuf = (const char*)cbuf;
+  a.P = dm->N + 1;
+  a.M = dm->M;
+  a.d = a.P * dm->n;
+  a.NT = NT;
+  a.ntiles = NT * (NT + 1) / 2;
+  a.q = dm->q;
+  a.has_prior = dm->has_prior;
+  for (int i = 0; i < 8; ++i) a.idx[i] = dm->meas_idx[i];
+  a.alpha = 2.0 / dm->T;
+  return a;
+}
+
+struct BuildCC {
+  const mhe_dims* dm;
+  int NT;
+  const double *D, *cw, *Phi, *Qw, *Rw, *Pw;
+  char* cb;
+  hipStream_t st;
+  template <class DYN, class MEAS>
+  int run() { return launch_cc<MEAS>(dm, NT, D, cw, Phi, Qw, Rw, Pw, cb, st); }
+};
+
+struct LaunchGN {
+  const mhe_dims* dm;
+  GnArgs* a;
+  int batch, mode;
+  hipStream_t st;
+  template <class DYN, class MEAS>
+  int run() { return launch_gn<DYN, MEAS>(dm, *a, batch, mode, st); }
+};
+
+}  // namespace
+
+extern "C" {
+
+const char* mhe_version(void) { return "libmhe 0.1 (gfx950, register-tiled fp64 MFMA Cholesky)"; }
+
+int32_t mhe_padded_dim(const mhe_dims* dims) {
+  int NT = 0;
+  if (check_dims(dims, &NT) != MHE_OK) return -1;
+  return 16 * NT;
+}
+
+size_t mhe_const_bytes(const mhe_dims* dims) {
+  int NT = 0;
+  if (check_dims(dims, &NT) != MHE_OK) return 0;
+  return const_layout(dims->N + 1, dims->M, dims->n, dims->p, NT).total;
+}
+
+int mhe_build_constants(const mhe_dims* dims, const double* D, const double* cw, const double* Phi,
+                        const double* Qw, const double* Rw, const double* Pw, void* const_buf, void* stream) {
+  int NT = 0;
+  int rc = check_dims(dims, &NT);
+  if (rc != MHE_OK) return rc;
+  if (!D || !cw || !Qw || !const_buf || (dims->M > 0 && (!Phi || !Rw)) || (dims->has_prior && !Pw))
+    return MHE_ERR_NULL;
+  hipStream_t st = (hipStream_t)stream;
+  BuildCC f{dims, NT, D, cw, Phi, Qw, Rw, Pw, (char*)const_buf, st};
+  return dispatch(dims, f);
+}
+
+int mhe_gn_solve(const mhe_dims* dims, const void* const_buf, int32_t batch, const double* X0, double* X_out,
+                 const double* U, int64_t u_bstride, const double* Y, const double* PAR, int64_t par_bstride,
+                 const double* x0, double* cost_out, int32_t* iters_out, int32_t* status_out, int32_t max_iter,
+                 double tol, void* stream) {
+  int NT = 0;
+  int rc = check_dims(dims, &NT);
+  if (rc != MHE_OK) return rc;
+  if (batch < 0 || max_iter < 0) return MHE_ERR_DIMS;
+  if (batch == 0) return MHE_OK;
+  if (!const_buf || !X0 || !X_out || !cost_out || !iters_out || !status_out || (dims->M > 0 && !Y) ||
+      (dims->m > 0 && !U) || (dims->q > 0 && !PAR) || (dims->has_prior && !x0))
+    return MHE_ERR_NULL;
+  GnArgs a = make_args(dims, const_buf, NT);
+  a.X0 = X0; a.Xout = X_out; a.U = U; a.ustride = u_bstride; a.Y = Y; a.PAR = PAR; a.pstride = par_bstride;
+  a.x0 = x0; a.cost = cost_out; a.iters = iters_out; a.status = status_out; a.max_iter = max_iter; a.tol = tol;
+  LaunchGN f{dims, &a, batch, MODE_SOLVE, (hipStream_t)stream};
+  return dispatch(dims, f);
+}
+
+int mhe_assemble(const mhe_dims* dims, const void* const_buf, int32_t batch, const double* X, const double* U,
+                 int64_t u_bstride, const double* Y, const double* PAR, int64_t par_bstride, const double* x0,
+                 double* H, double* g, double* cost, void* stream) {
+  int NT = 0;
+  int rc = check_dims(dims, &NT);
+  if (rc != MHE_OK) return rc;
+  if (batch <= 0) return batch == 0 ? MHE_OK : MHE_ERR_DIMS;
+  if (!const_buf || !X || !H || !g || !cost || (dims->M > 0 && !Y) || (dims->m > 0 && !U) ||
+      (dims->q > 0 && !PAR) || (dims->has_prior && !x0))
+    return MHE_ERR_NULL;
+  GnArgs a = make_args(dims, const_buf, NT);
+  a.X0 = X; a.U = U; a.ustride = u_bstride; a.Y = Y; a.PAR = PAR; a.pstride = par_bstride; a.x0 = x0;
+  a.Hout = H; a.gout = g; a.cost = cost;
+  LaunchGN f{dims, &a, batch, MODE_ASSEMBLE, (hipStream_t)stream};
+  return dispatch(dims, f);
+}
+
+int mhe_chol_solve(const mhe_dims* dims, const void* const_buf, int32_t batch, const double* H, const double* g,
+                   double* delta, int32_t* status, void* stream) {
+  int NT = 0;
+  int rc = check_dims(dims, &NT);
+  if (rc != MHE_OK) return rc;
+  if (batch <= 0) return batch == 0 ? MHE_OK : MHE_ERR_DIMS;
+  if (!const_buf || !H || !g || !delta || !status) return MHE_ERR_NULL;
+  GnArgs a = make_args(dims, const_buf, NT);
+  a.Hin = H; a.gin = g; a.dout = delta; a.status = status;
+  LaunchGN f{dims, &a, batch, MODE_LINSOLVE, (hipStream_t)stream};
+  return dispatch(dims, f);
+}
+
+}  // extern "C"

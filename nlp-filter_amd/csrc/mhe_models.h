@@ -1,0 +1,176 @@
+// Device functors for the reference plug-ins (nlp/dynamics.py, nlp/measurements.py).
+//
+// Each dynamics functor: static n, m; eval(x, u, f, F) writes f (n) and the
+// Jacobian F = df/dx (n*n, row-major).  Each measurement functor: static p,
+// q, LINEAR; eval(x, par, idx, h, H) writes h (p) and H = dh/dx (p*n).
+// Jacobians are analytic; their parity against the reference's own plug-ins
+// (complex-step through the reference code) is pinned by tests/golden/plugins.npz.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace mhe {
+
+// nlp/dynamics.py:4-8  xdot = u[0]
+struct DynSingleIntegrator {
+  static constexpr int n = 1, m = 1;
+  __device__ static void eval(const double* x, const double* u, double* f, double* F) {
+    f[0] = u[0];
+    F[0] = 0.0;
+  }
+};
+
+// nlp/dynamics.py:10-27  xdot = u
+template <int N_>
+struct DynSingleIntegratorND {
+  static constexpr int n = N_, m = N_;
+  __device__ static void eval(const double* x, const double* u, double* f, double* F) {
+#pragma unroll
+    for (int a = 0; a < n; ++a) {
+      f[a] = u[a];
+#pragma unroll
+      for (int b = 0; b < n; ++b) F[a * n + b] = 0.0;
+    }
+  }
+};
+
+// nlp/dynamics.py:29-38
+struct DynDoubleIntegrator {
+  static constexpr int n = 4, m = 2;
+  __device__ static void eval(const double* x, const double* u, double* f, double* F) {
+    f[0] = x[2]; f[1] = x[3]; f[2] = u[0]; f[3] = u[1];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) F[i] = 0.0;
+    F[0 * 4 + 2] = 1.0;
+    F[1 * 4 + 3] = 1.0;
+  }
+};
+
+// nlp/dynamics.py:61-66  [(1 - x1^2) x0 - x1 + u, x0]
+struct DynVanDerPol {
+  static constexpr int n = 2, m = 1;
+  __device__ static void eval(const double* x, const double* u, double* f, double* F) {
+    const double x0 = x[0], x1 = x[1];
+    const double s = 1.0 - x1 * x1;
+    f[0] = s * x0 - x1 + u[0];
+    f[1] = x0;
+    F[0] = s;
+    F[1] = -2.0 * x1 * x0 - 1.0;
+    F[2] = 1.0;
+    F[3] = 0.0;
+  }
+};
+
+// nlp/dynamics.py:68-79  [u0, u1, u2, x4, 0]
+struct DynGnssPosAndBias {
+  static constexpr int n = 5, m = 3;
+  __device__ static void eval(const double* x, const double* u, double* f, double* F) {
+    f[0] = u[0]; f[1] = u[1]; f[2] = u[2]; f[3] = x[4]; f[4] = 0.0;
+#pragma unroll
+    for (int i = 0; i < 25; ++i) F[i] = 0.0;
+    F[3 * 5 + 4] = 1.0;
+  }
+};
+
+// nlp/dynamics.py:81-96 (m = 0: f(x, params), nlp/nlp.py:216-219)
+struct DynMultiReceiver {
+  static constexpr int n = 8, m = 0;
+  __device__ static void eval(const double* x, const double*, double* f, double* F) {
+#pragma unroll
+    for (int i = 0; i < 64; ++i) F[i] = 0.0;
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      f[a] = x[a + 4];
+      f[a + 4] = 0.0;
+      F[a * 8 + a + 4] = 1.0;
+    }
+  }
+};
+
+// nlp/dynamics.py:98-115
+struct DynGnssTwoReceiver {
+  static constexpr int n = 10, m = 6;
+  __device__ static void eval(const double* x, const double* u, double* f, double* F) {
+    f[0] = u[0]; f[1] = u[1]; f[2] = u[2]; f[3] = x[4]; f[4] = 0.0;
+    f[5] = u[3]; f[6] = u[4]; f[7] = u[5]; f[8] = x[9]; f[9] = 0.0;
+#pragma unroll
+    for (int i = 0; i < 100; ++i) F[i] = 0.0;
+    F[3 * 10 + 4] = 1.0;
+    F[8 * 10 + 9] = 1.0;
+  }
+};
+
+// nlp/dynamics.py:117-136 (kinematic_bycicle_and_bias; the reference code uses
+// x[2] as the heading inside cos/sin, reproduced verbatim)
+struct DynKinematicBicycle {
+  static constexpr int n = 6, m = 2;
+  __device__ static void eval(const double* x, const double* u, double* f, double* F) {
+    const double L = 0.28;
+    const double v = 8.72649116358 * u[0] - 0.856053299155;
+    const double delta = 0.48869219055841229 * u[1];  // np.deg2rad(28)
+    double sn, cs;
+    sincos(x[2], &sn, &cs);
+    f[0] = v * cs; f[1] = v * sn; f[2] = 0.0; f[3] = x[4]; f[4] = 0.0;
+    f[5] = (v / L) * tan(delta);
+#pragma unroll
+    for (int i = 0; i < 36; ++i) F[i] = 0.0;
+    F[0 * 6 + 2] = -v * sn;
+    F[1 * 6 + 2] = v * cs;
+    F[3 * 6 + 4] = 1.0;
+  }
+};
+
+// ---------------------------------------------------------------- measurements
+
+// nlp/measurements.py:4-5  h = x (linear: its Gauss-Newton Hessian term is constant)
+template <int N_>
+struct MeasFullState {
+  static constexpr int p = N_, q = 0;
+  static constexpr bool LINEAR = true;
+  __device__ static void eval(const double* x, const double*, const int*, double* h, double* H) {
+#pragma unroll
+    for (int a = 0; a < p; ++a) {
+      h[a] = x[a];
+#pragma unroll
+      for (int b = 0; b < p; ++b) H[a * p + b] = (a == b) ? 1.0 : 0.0;
+    }
+  }
+};
+
+// nlp/measurements.py:56-70  ||x[idx0:3] - sat|| + x[idx3]
+template <int N_>
+struct MeasPseudorange {
+  static constexpr int p = 1, q = 3;
+  static constexpr bool LINEAR = false;
+  __device__ static void eval(const double* x, const double* par, const int* idx, double* h, double* H) {
+    const double d0 = x[idx[0]] - par[0], d1 = x[idx[1]] - par[1], d2 = x[idx[2]] - par[2];
+    const double rho = sqrt(d0 * d0 + d1 * d1 + d2 * d2);
+    h[0] = rho + x[idx[3]];
+#pragma unroll
+    for (int a = 0; a < N_; ++a) H[a] = 0.0;
+    const double ir = 1.0 / rho;
+    H[idx[0]] += d0 * ir;
+    H[idx[1]] += d1 * ir;
+    H[idx[2]] += d2 * ir;
+    H[idx[3]] += 1.0;
+  }
+};
+
+// nlp/measurements.py:39-54  ("y" form) sqrt(sum (x[idx] - y)^2 + 1e-6)
+template <int N_>
+struct MeasRange3D {
+  static constexpr int p = 1, q = 3;
+  static constexpr bool LINEAR = false;
+  __device__ static void eval(const double* x, const double* par, const int* idx, double* h, double* H) {
+    const double d0 = x[idx[0]] - par[0], d1 = x[idx[1]] - par[1], d2 = x[idx[2]] - par[2];
+    const double r = sqrt(d0 * d0 + d1 * d1 + d2 * d2 + 0.000001);
+    h[0] = r;
+#pragma unroll
+    for (int a = 0; a < N_; ++a) H[a] = 0.0;
+    const double ir = 1.0 / r;
+    H[idx[0]] += d0 * ir;
+    H[idx[1]] += d1 * ir;
+    H[idx[2]] += d2 * ir;
+  }
+};
+
+}  // namespace mhe

@@ -1,0 +1,81 @@
+"""ctypes binding of libmhe.so (the C-ABI declared in include/mhe.h).
+
+The library is built in-tree (``python __graft_entry__.py`` / ``make -C
+nlp-filter_amd/csrc``) to ``nlp-filter_amd/mhe/libmhe.so``.  There is no CPU
+fallback: if the library is missing or fails to load, every solver entry point
+raises ``MheLibraryError``.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("MHE_LIB", os.path.join(HERE, "libmhe.so"))
+
+MHE_OK = 0
+ERRORS = {-1: "MHE_ERR_DIMS", -2: "MHE_ERR_MODEL", -3: "MHE_ERR_HIP", -4: "MHE_ERR_UNSUPPORTED", -5: "MHE_ERR_NULL"}
+STATUS = {0: "converged", 1: "max_iter", 2: "not_spd", 3: "nonfinite"}
+
+# symbol -> (restype, argtypes); must match include/mhe.h exactly
+c_i32, c_i64, c_dbl, c_vp, c_sz = ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p, ctypes.c_size_t
+
+
+class MheDims(ctypes.Structure):
+    _fields_ = [
+        ("N", c_i32), ("n", c_i32), ("m", c_i32), ("p", c_i32), ("M", c_i32), ("q", c_i32),
+        ("dyn_model", c_i32), ("meas_model", c_i32), ("has_prior", c_i32),
+        ("meas_idx", c_i32 * 8), ("T", c_dbl),
+    ]
+
+
+_P = ctypes.POINTER(MheDims)
+SIGNATURES = {
+    "mhe_version": (ctypes.c_char_p, []),
+    "mhe_padded_dim": (c_i32, [_P]),
+    "mhe_const_bytes": (c_sz, [_P]),
+    "mhe_build_constants": (ctypes.c_int, [_P, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "mhe_gn_solve": (ctypes.c_int, [_P, c_vp, c_i32, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp,
+                                    c_vp, c_vp, c_vp, c_i32, c_dbl, c_vp]),
+    "mhe_assemble": (ctypes.c_int, [_P, c_vp, c_i32, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp,
+                                    c_vp, c_vp, c_vp, c_vp]),
+    "mhe_chol_solve": (ctypes.c_int, [_P, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
+}
+
+
+class MheLibraryError(RuntimeError):
+    pass
+
+
+class MheCallError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load(path=None):
+    """Load libmhe.so once (raises MheLibraryError if absent)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise MheLibraryError(
+            f"libmhe.so not found at {p}: build it with `python __graft_entry__.py` "
+            "(hipcc --offload-arch=gfx950). There is no CPU fallback.")
+    try:
+        import torch  # noqa: F401  (bind to the HIP runtime torch already loaded)
+    except Exception:
+        pass
+    lib = ctypes.CDLL(p)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def check(rc, what):
+    if rc != MHE_OK:
+        raise MheCallError(f"{what} failed: {ERRORS.get(rc, rc)}")

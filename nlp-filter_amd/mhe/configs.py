@@ -1,0 +1,137 @@
+"""Seeded synthetic workloads for the BASELINE.json configs.
+
+Host-side data generation only (truth by fixed-step RK4, noise by
+``numpy.random.default_rng(seed)``, draws in batch order).  Nothing here is on
+the timed path.
+
+C1  single_integrator: n=1, m=1, full_state, N=20, T=10, M=50, B=1
+    (estimation_example.py:13,20,24,33 scales; u = sin t)
+C2  van_der_pol:       n=2, m=1 (u = 0), full_state, N=100, T=10, M=101, B=1024
+    (van_der_pol.py:10,33 scales; R, Q from estimation_example.py:20,33)
+"""
+import numpy as np
+from scipy.interpolate import interp1d
+
+from nlp.collocation import ChebyshevPseudospectralMethod
+
+
+class Workload:
+    """Everything one batched estimation solve needs (numpy, host)."""
+
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+    @property
+    def P(self):
+        return self.N + 1
+
+
+def _rk4(f, x0, t, substeps=20):
+    """Fixed-step RK4 over sample times t for a batch x0 (B, n)."""
+    out = np.zeros((x0.shape[0], t.shape[0], x0.shape[1]))
+    x = x0.copy()
+    out[:, 0] = x
+    for i in range(1, t.shape[0]):
+        h = (t[i] - t[i - 1]) / substeps
+        tt = t[i - 1]
+        for _ in range(substeps):
+            k1 = f(tt, x)
+            k2 = f(tt + h / 2, x + h / 2 * k1)
+            k3 = f(tt + h / 2, x + h / 2 * k2)
+            k4 = f(tt + h, x + h * k3)
+            x = x + h / 6 * (k1 + 2 * k2 + 2 * k3 + k4)
+            tt += h
+        out[:, i] = x
+    return out
+
+
+def _init_from_measurements(cpm, t_meas, Y):
+    """initializeEstimate (nlp/nlp.py:288-302) applied to y for every trajectory."""
+    t_nodes = cpm.tau2t(cpm.tau)
+    X = np.zeros((Y.shape[0], t_nodes.shape[0], Y.shape[2]))
+    for b in range(Y.shape[0]):
+        X[b] = interp1d(t_meas, Y[b].T, fill_value="extrapolate")(t_nodes).T
+    return X
+
+
+def make_c1(seed=0, B=1, N=20):
+    T, M = 10.0, 50
+    rng = np.random.default_rng(seed)
+    t = np.linspace(0, T, M)
+    u = np.sin(t)
+    cpm = ChebyshevPseudospectralMethod(N, 0, T)
+    x0 = np.zeros((B, 1))
+    # single integrator: x(t) = int_0^t sin = 1 - cos t
+    xt = x0[:, None, :] + (1 - np.cos(t))[None, :, None]
+    R = np.array([[0.01]])
+    Y = xt + rng.normal(size=xt.shape) * np.sqrt(R[0, 0])
+    t_nodes = cpm.tau2t(cpm.tau)
+    U = interp1d(t, u[None, :], fill_value="extrapolate")(t_nodes).T[None]  # (1, P, 1)
+    Q = np.array([[1e-4]])
+    return Workload(name="C1_single_integrator", N=N, T=T, n=1, m=1, p=1, M=M, B=B,
+                    dyn="single_integrator", meas="full_state", meas_static={},
+                    t_meas=t, Y=Y, U=U, PAR=None, Qw=np.linalg.inv(Q),
+                    Rw=np.broadcast_to(np.linalg.inv(R), (M, 1, 1)).copy(), Pw=None, x0=None,
+                    X_init=_init_from_measurements(cpm, t, Y), X_true=xt, cpm=cpm)
+
+
+def vdp_rhs(t, x):
+    return np.stack([(1 - x[:, 1] ** 2) * x[:, 0] - x[:, 1], x[:, 0]], axis=1)
+
+
+def make_c2(B=1024, seed=1, N=100):
+    T, M = 10.0, 101
+    rng = np.random.default_rng(seed)
+    x0 = np.array([0.0, 1.0])[None, :] + rng.normal(size=(B, 2)) * 0.1
+    t = np.linspace(0, T, M)
+    xt = _rk4(vdp_rhs, x0, t)
+    R = np.diag([0.01, 0.02])
+    Y = xt + rng.normal(size=xt.shape) * np.sqrt(np.diag(R))[None, None, :]
+    cpm = ChebyshevPseudospectralMethod(N, 0, T)
+    Q = np.diag([1e-4, 1e-4])
+    return Workload(name="C2_van_der_pol", N=N, T=T, n=2, m=1, p=2, M=M, B=B,
+                    dyn="van_der_pol", meas="full_state", meas_static={},
+                    t_meas=t, Y=Y, U=np.zeros((1, N + 1, 1)), PAR=None, Qw=np.linalg.inv(Q),
+                    Rw=np.broadcast_to(np.linalg.inv(R), (M, 2, 2)).copy(), Pw=None, x0=None,
+                    X_init=_init_from_measurements(cpm, t, Y), X_true=xt, cpm=cpm)
+
+
+CONFIGS = {"C1": make_c1, "C2": make_c2}
+
+
+def make_gnss_small(B=4, seed=2, N=10, T=50.0, n_sat=8, epochs=51):
+    """Small gnss_stationary-shaped problem (pseudorange, n=5) for parity tests.
+
+    Synthetic ENU satellite positions at ~2e7 m (fixed per slot over the
+    window, shared by the batch); truth = stationary receiver + drifting clock.
+    Q, r_pr as gnss_stationary.py:18-19.
+    """
+    rng = np.random.default_rng(seed)
+    t_ep = np.linspace(0, T, epochs)
+    az = rng.uniform(0, 2 * np.pi, n_sat)
+    el = rng.uniform(0.3, 1.3, n_sat)
+    sat = 2.2e7 * np.stack([np.cos(el) * np.cos(az), np.cos(el) * np.sin(az), np.sin(el)], axis=1)
+    t_meas = np.repeat(t_ep, n_sat)
+    PAR = np.tile(sat, (epochs, 1))[None]  # (1, M, 3)
+    M = t_meas.shape[0]
+    pos = rng.normal(size=(B, 3)) * 10.0
+    b0 = rng.normal(size=B) * 100.0
+    bd = rng.normal(size=B) * 0.5
+    r_pr = 100.0
+    xt = np.zeros((B, epochs, 5))
+    xt[:, :, :3] = pos[:, None, :]
+    xt[:, :, 3] = b0[:, None] + bd[:, None] * t_ep[None, :]
+    xt[:, :, 4] = bd[:, None]
+    rho = np.linalg.norm(xt[:, :, None, :3] - sat[None, None, :, :], axis=-1) + xt[:, :, None, 3]
+    Y = (rho + rng.normal(size=rho.shape) * np.sqrt(r_pr)).reshape(B, M, 1)
+    cpm = ChebyshevPseudospectralMethod(N, 0, T)
+    t_nodes = cpm.tau2t(cpm.tau)
+    X_init = np.zeros((B, N + 1, 5))
+    X_init[:, :, :3] = pos[:, None, :] + rng.normal(size=(B, 1, 3)) * 3.0
+    X_init[:, :, 3] = (b0[:, None] + bd[:, None] * t_nodes[None, :]) + rng.normal(size=(B, 1)) * 3.0
+    X_init[:, :, 4] = bd[:, None]
+    Q = np.diag([0.0001, 0.0001, 0.0001, 0.1, 0.001])
+    return Workload(name="gnss_small", N=N, T=T, n=5, m=3, p=1, M=M, B=B,
+                    dyn="gnss_pos_and_bias", meas="pseudorange", meas_static={"idx": [0, 1, 2, 3]},
+                    t_meas=t_meas, Y=Y, U=np.zeros((1, N + 1, 3)), PAR=PAR, Qw=np.linalg.inv(Q),
+                    Rw=np.full((M, 1, 1), 1.0 / r_pr), Pw=None, x0=None, X_init=X_init, X_true=xt, cpm=cpm)

@@ -1,0 +1,190 @@
+"""Batched Gauss-Newton solver on libmhe.so (device-resident, torch as container).
+
+``BatchSolver`` owns the device constants of one problem structure (N, T,
+models, measurement times, weights) and solves many independent trajectories
+that share it:  X (B, P, n), U (B|1, P, m), Y (B, M, p), PAR (B|1, M, q),
+x0 (B, n).  Everything is fp64 and stays in HBM between calls; the HIP work is
+enqueued on the current torch stream (or the one passed in).
+"""
+import numpy as np
+import torch
+
+from . import _lib, registry
+
+STATUS_CONVERGED, STATUS_MAX_ITER, STATUS_NOT_SPD, STATUS_NONFINITE = 0, 1, 2, 3
+
+
+def _dev(x, device, shape=None):
+    if x is None:
+        return None
+    if isinstance(x, torch.Tensor):
+        t = x.to(device=device, dtype=torch.float64)
+    else:
+        t = torch.as_tensor(np.asarray(x, dtype=np.float64), device=device)
+    t = t.contiguous()
+    if shape is not None and tuple(t.shape) != tuple(shape):
+        raise ValueError(f"expected shape {shape}, got {tuple(t.shape)}")
+    return t
+
+
+def _ptr(t):
+    return None if t is None else ctypes_ptr(t)
+
+
+def ctypes_ptr(t):
+    import ctypes
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _stream(stream):
+    import ctypes
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+class BatchSolver:
+    """Device constants + launch wrappers for one problem structure.
+
+    Parameters (host numpy or torch):
+      N, T            collocation order and window length
+      dyn, meas       plug-in functions (or names) -- see mhe.registry
+      D (P,P), cw (P) differentiation matrix, (T/2) * quadrature weights
+      Phi (M,P)       Lagrange basis at the measurement times
+      Qw (n,n)        dynamics-cost information (weighted_l2_norm params["Q"])
+      Rw (M,p,p)      measurement information (R passed to addResidualCost)
+      Pw (n,n)|None   prior information (addInitialCost), None = no prior
+      meas_idx        static index parameters of the measurement model
+    """
+
+    def __init__(self, N, T, dyn, meas, D, cw, Phi, Qw, Rw, Pw=None, meas_idx=None, device="cuda"):
+        self.lib = _lib.load()
+        if not torch.cuda.is_available():
+            raise _lib.MheLibraryError("no HIP device visible: the estimator has no CPU path")
+        self.device = torch.device(device)
+        dname, (did, n, m) = registry.dyn_model(dyn)
+        mname, (mid, p, q, linear) = registry.meas_model(meas)
+        registry.check_pair(dname, mname)
+        p = n if p is None else p
+        self.N, self.T, self.n, self.m, self.p, self.q = int(N), float(T), n, m, p, q
+        self.P = self.N + 1
+        Phi = np.asarray(Phi, dtype=np.float64).reshape(-1, self.P)
+        self.M = Phi.shape[0]
+        self.dyn_name, self.meas_name, self.linear_meas = dname, mname, linear
+        dims = _lib.MheDims()
+        dims.N, dims.n, dims.m, dims.p, dims.M, dims.q = self.N, n, m, p, self.M, q
+        dims.dyn_model, dims.meas_model = did, mid
+        dims.has_prior = 0 if Pw is None else 1
+        idx = list(meas_idx) if meas_idx is not None else ([0, 1, 2, 3] if mname != "vehicle_pseudorange" else [0, 1, 8, 6])
+        for i in range(8):
+            dims.meas_idx[i] = idx[i] if i < len(idx) else 0
+        dims.T = self.T
+        self.dims = dims
+        self.dp = self.lib.mhe_padded_dim(dims)
+        if self.dp < 0:
+            raise _lib.MheCallError("mhe_padded_dim: unsupported dims (system too large for this build?)")
+        nbytes = self.lib.mhe_const_bytes(dims)
+        if nbytes == 0:
+            raise _lib.MheCallError("mhe_const_bytes: invalid dims")
+        dev = self.device
+        self._host = dict(D=np.asarray(D, np.float64), cw=np.asarray(cw, np.float64), Phi=Phi,
+                          Qw=np.asarray(Qw, np.float64), Rw=np.asarray(Rw, np.float64).reshape(self.M, p, p),
+                          Pw=None if Pw is None else np.asarray(Pw, np.float64))
+        self._src = {k: _dev(v, dev) for k, v in self._host.items() if v is not None}
+        self.cbuf = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        Pw_t = self._src.get("Pw")
+        rc = self.lib.mhe_build_constants(
+            self.dims, _ptr(self._src["D"]), _ptr(self._src["cw"]), _ptr(self._src["Phi"]),
+            _ptr(self._src["Qw"]), _ptr(self._src["Rw"]), _ptr(Pw_t), _ptr(self.cbuf), _stream(None))
+        _lib.check(rc, "mhe_build_constants")
+
+    # ------------------------------------------------------------------ inputs
+    def _inputs(self, X, U, Y, PAR, x0):
+        dev = self.device
+        X = _dev(X, dev)
+        if X.dim() != 3 or X.shape[1:] != (self.P, self.n):
+            raise ValueError(f"X must be (B, {self.P}, {self.n}), got {tuple(X.shape)}")
+        B = X.shape[0]
+        U_t, ustr = None, 0
+        if self.m > 0:
+            if U is None:
+                raise ValueError("controls U are required for this dynamics model")
+            U_t = _dev(U, dev)
+            if U_t.dim() == 2:
+                U_t = U_t[None]
+            if U_t.shape[1:] != (self.P, self.m) or U_t.shape[0] not in (1, B):
+                raise ValueError(f"U must be (B|1, {self.P}, {self.m}), got {tuple(U_t.shape)}")
+            ustr = 0 if U_t.shape[0] == 1 else self.P * self.m
+        Y_t = _dev(Y, dev, (B, self.M, self.p))
+        PAR_t, pstr = None, 0
+        if self.q > 0:
+            PAR_t = _dev(PAR, dev)
+            if PAR_t.dim() == 2:
+                PAR_t = PAR_t[None]
+            if PAR_t.shape[1:] != (self.M, self.q) or PAR_t.shape[0] not in (1, B):
+                raise ValueError(f"PAR must be (B|1, {self.M}, {self.q}), got {tuple(PAR_t.shape)}")
+            pstr = 0 if PAR_t.shape[0] == 1 else self.M * self.q
+        x0_t = None
+        if self.dims.has_prior:
+            x0_t = _dev(x0, dev, (B, self.n))
+        return X, B, U_t, ustr, Y_t, PAR_t, pstr, x0_t
+
+    # ------------------------------------------------------------------ calls
+    def solve(self, X0, U, Y, PAR=None, x0=None, max_iter=20, tol=1e-10, stream=None, out=None):
+        """Gauss-Newton to convergence. Returns (X, cost, iters, status) device tensors."""
+        X, B, U_t, ustr, Y_t, PAR_t, pstr, x0_t = self._inputs(X0, U, Y, PAR, x0)
+        if out is None:
+            Xo = torch.empty_like(X)
+            cost = torch.empty(B, dtype=torch.float64, device=self.device)
+            iters = torch.empty(B, dtype=torch.int32, device=self.device)
+            status = torch.empty(B, dtype=torch.int32, device=self.device)
+        else:
+            Xo, cost, iters, status = out
+        rc = self.lib.mhe_gn_solve(self.dims, _ptr(self.cbuf), B, _ptr(X), _ptr(Xo), _ptr(U_t), ustr, _ptr(Y_t),
+                                   _ptr(PAR_t), pstr, _ptr(x0_t), _ptr(cost), _ptr(iters), _ptr(status),
+                                   int(max_iter), float(tol), _stream(stream))
+        _lib.check(rc, "mhe_gn_solve")
+        return Xo, cost, iters, status
+
+    def prepare(self, X0, U, Y, PAR=None, x0=None):
+        """Pre-stage device inputs once (bench: inputs resident before timing)."""
+        return self._inputs(X0, U, Y, PAR, x0)
+
+    def solve_staged(self, staged, outs, max_iter, tol, stream=None):
+        X, B, U_t, ustr, Y_t, PAR_t, pstr, x0_t = staged
+        Xo, cost, iters, status = outs
+        rc = self.lib.mhe_gn_solve(self.dims, _ptr(self.cbuf), B, _ptr(X), _ptr(Xo), _ptr(U_t), ustr, _ptr(Y_t),
+                                   _ptr(PAR_t), pstr, _ptr(x0_t), _ptr(cost), _ptr(iters), _ptr(status),
+                                   int(max_iter), float(tol), _stream(stream))
+        _lib.check(rc, "mhe_gn_solve")
+
+    def assemble(self, X, U, Y, PAR=None, x0=None, stream=None):
+        """GN normal equations at X: H (B,dp,dp), g (B,dp), cost (B)."""
+        X, B, U_t, ustr, Y_t, PAR_t, pstr, x0_t = self._inputs(X, U, Y, PAR, x0)
+        H = torch.empty((B, self.dp, self.dp), dtype=torch.float64, device=self.device)
+        g = torch.empty((B, self.dp), dtype=torch.float64, device=self.device)
+        cost = torch.empty(B, dtype=torch.float64, device=self.device)
+        rc = self.lib.mhe_assemble(self.dims, _ptr(self.cbuf), B, _ptr(X), _ptr(U_t), ustr, _ptr(Y_t), _ptr(PAR_t),
+                                   pstr, _ptr(x0_t), _ptr(H), _ptr(g), _ptr(cost), _stream(stream))
+        _lib.check(rc, "mhe_assemble")
+        return H, g, cost
+
+    def chol_solve(self, H, g, stream=None):
+        """delta = -H^{-1} g with the solver's tiled Cholesky (H: (B,dp,dp) SPD)."""
+        H = _dev(H, self.device)
+        g = _dev(g, self.device)
+        B = H.shape[0]
+        if H.shape[1:] != (self.dp, self.dp) or g.shape != (B, self.dp):
+            raise ValueError(f"H must be (B,{self.dp},{self.dp}) and g (B,{self.dp})")
+        delta = torch.empty((B, self.dp), dtype=torch.float64, device=self.device)
+        status = torch.empty(B, dtype=torch.int32, device=self.device)
+        rc = self.lib.mhe_chol_solve(self.dims, _ptr(self.cbuf), B, _ptr(H), _ptr(g), _ptr(delta), _ptr(status),
+                                     _stream(stream))
+        _lib.check(rc, "mhe_chol_solve")
+        return delta, status
+
+
+def from_workload(w, device="cuda"):
+    """BatchSolver for a mhe.configs.Workload."""
+    Phi = w.cpm.lagrange_matrix(w.t_meas)
+    return BatchSolver(w.N, w.T, w.dyn, w.meas, w.cpm.D, (w.T / 2.0) * w.cpm.w, Phi, w.Qw, w.Rw,
+                       Pw=w.Pw, meas_idx=w.meas_static.get("idx"), device=device)

@@ -1,0 +1,189 @@
+"""Oracle: the estimation objective and a batched Gauss-Newton solver -- TEST INFRASTRUCTURE ONLY.
+
+Restates the objective that ``fixedTimeOptimalEstimationNLP`` hands to IPOPT,
+with the process-noise variables W eliminated through the collocation equality:
+
+  W_k(X) = (2/T) sum_j D_kj X_j - f(X_k, U_k)            nlp/nlp.py:225-235
+  J_dyn  = sum_k (T/2) w_k  W_k^T Qw W_k                  nlp/nlp.py:242-245, cost_functions.py:20-22
+  J_meas = sum_i e_i^T Rw_i e_i,  e_i = y_i - h(X(t_i))   nlp/nlp.py:264-273 (R passed as information)
+           X(t_i) = sum_j phi_j(t_i) X_j                  nlp/nlp.py:266-269
+  J_0    = (X_0 - x0)^T Pw (X_0 - x0)                     nlp/nlp.py:279-286
+
+Gauss-Newton on J (the same stationary point IPOPT returns for this
+unconstrained problem): H delta = -g with H = sum A^T W A, g = sum A^T W r.
+
+Two independent forms are provided:
+  * ``normal_equations``          structured (Kronecker) form, vectorised over the batch
+                                  -- also the CPU-baseline workload of bench.py;
+  * ``normal_equations_explicit`` builds the stacked Jacobian row by row from the
+                                  reference's per-node / per-measurement expressions.
+"""
+import numpy as np
+
+from . import models
+
+OK, MAXITER, NOT_SPD, NONFINITE = 0, 1, 2, 3
+
+
+class Problem:
+    """Structure shared by every trajectory of a batch (plain container)."""
+
+    def __init__(self, N, T, n, m, dyn, meas, D, c, Phi, Qw, Rw, Pw=None, meas_static=None):
+        self.N, self.T, self.n, self.m = N, float(T), n, m
+        self.P = N + 1
+        self.d = self.P * n
+        self.alpha = 2.0 / float(T)
+        self.dyn, self.meas = dyn, meas
+        self.meas_static = meas_static or {}
+        self.D = np.asarray(D, dtype=np.float64)
+        self.c = np.asarray(c, dtype=np.float64)          # (T/2) w_k
+        self.Phi = np.asarray(Phi, dtype=np.float64)      # (M, P)
+        self.Qw = np.asarray(Qw, dtype=np.float64)        # (n, n)
+        self.Rw = np.asarray(Rw, dtype=np.float64)        # (M, p, p) or (B, M, p, p)
+        self.Pw = None if Pw is None else np.asarray(Pw, dtype=np.float64)
+        self.M = self.Phi.shape[0]
+
+
+def residuals(pb, X, U, Y, PAR=None, x0=None):
+    """Return W (B,P,n), xi (B,M,n), e (B,M,p), cost (B,)."""
+    X = np.asarray(X, dtype=np.float64)
+    DX = np.einsum("kj,bja->bka", pb.D, X)
+    f, _ = models.dyn_eval(pb.dyn, X, U)
+    W = pb.alpha * DX - f
+    cost = np.einsum("k,bka,ac,bkc->b", pb.c, W, pb.Qw, W)
+    xi = np.einsum("ij,bja->bia", pb.Phi, X)
+    h, _ = models.meas_eval(pb.meas, xi, PAR, pb.meas_static)
+    e = Y - h
+    Rw = pb.Rw if pb.Rw.ndim == 4 else pb.Rw[None]
+    cost = cost + np.einsum("bip,bipq,biq->b", e, np.broadcast_to(Rw, e.shape + (e.shape[-1],)), e)
+    if pb.Pw is not None:
+        r0 = X[:, 0] - x0
+        cost = cost + np.einsum("ba,ac,bc->b", r0, pb.Pw, r0)
+    return W, xi, e, cost
+
+
+def normal_equations(pb, X, U, Y, PAR=None, x0=None):
+    """Structured GN normal equations. Returns H (B,d,d), g (B,d), cost (B,)."""
+    X = np.asarray(X, dtype=np.float64)
+    B, P, n = X.shape
+    W, xi, e, cost = residuals(pb, X, U, Y, PAR, x0)
+    _, F = models.dyn_eval(pb.dyn, X, U)
+    a = pb.alpha
+    # dynamics: block(j,l) = a^2 (D^T C D)_jl Qw - a D_lj E_l - a D_jl E_j^T + delta_jl F_j^T E_j
+    E = np.einsum("k,ac,zkce->zkae", pb.c, pb.Qw, F)              # c_k Qw F_k
+    DCD = np.einsum("kj,k,kl->jl", pb.D, pb.c, pb.D)
+    H4 = np.broadcast_to((a * a) * np.einsum("jl,ae->jale", DCD, pb.Qw), (B, P, n, P, n)).copy()
+    H4 -= a * np.einsum("lj,zlae->zjale", pb.D, E)
+    H4 -= a * np.einsum("jl,zjea->zjale", pb.D, E)
+    FtE = np.einsum("zjca,zjce->zjae", F, E)
+    for j in range(P):
+        H4[:, j, :, j, :] += FtE[:, j]
+    V = np.einsum("k,ac,zkc->zka", pb.c, pb.Qw, W)                # c_k Qw W_k
+    g = a * np.einsum("kj,zka->zja", pb.D, V) - np.einsum("zjca,zjc->zja", F, V)
+    # measurements
+    _, Hm = models.meas_eval(pb.meas, xi, PAR, pb.meas_static)    # (B,M,p,n)
+    Rw = pb.Rw if pb.Rw.ndim == 4 else np.broadcast_to(pb.Rw[None], (B,) + pb.Rw.shape)
+    G = np.einsum("zipa,zipq,ziqc->ziac", Hm, Rw, Hm)              # (B,M,n,n)
+    H4 += np.einsum("ij,il,ziac->zjalc", pb.Phi, pb.Phi, G)
+    ge = np.einsum("zipa,zipq,ziq->zia", Hm, Rw, e)
+    g -= np.einsum("ij,zia->zja", pb.Phi, ge)
+    if pb.Pw is not None:
+        H4[:, 0, :, 0, :] += pb.Pw
+        g[:, 0] += (X[:, 0] - x0) @ pb.Pw.T
+    d = P * n
+    return H4.reshape(B, d, d), g.reshape(B, d), cost
+
+
+def normal_equations_explicit(pb, X, U, Y, PAR=None, x0=None):
+    """Row-by-row stacked Jacobian (independent restatement; small problems only)."""
+    X = np.asarray(X, dtype=np.float64)
+    B, P, n = X.shape
+    d = P * n
+    Hs, gs, cs = [], [], []
+    for b in range(B):
+        rows, Ws, rs = [], [], []
+        for k in range(P):  # dynamics defect rows, nlp/nlp.py:225-235
+            fk, Fk = models.dyn_eval(pb.dyn, X[b, k], None if U is None else U[b, k])
+            Wk = pb.alpha * (pb.D[k] @ X[b]) - fk
+            A = np.zeros((n, d))
+            for j in range(P):
+                A[:, j * n:(j + 1) * n] += pb.alpha * pb.D[k, j] * np.eye(n)
+            A[:, k * n:(k + 1) * n] -= Fk
+            rows.append(A); Ws.append(pb.c[k] * pb.Qw); rs.append(Wk)
+        Rw = pb.Rw[b] if pb.Rw.ndim == 4 else pb.Rw
+        for i in range(pb.M):  # measurement rows, nlp/nlp.py:264-273
+            xi = pb.Phi[i] @ X[b]
+            par = None if PAR is None else PAR[min(b, PAR.shape[0] - 1), i]
+            hi, Hi = models.meas_eval(pb.meas, xi, par, pb.meas_static)
+            A = np.zeros((Hi.shape[0], d))
+            for j in range(P):
+                A[:, j * n:(j + 1) * n] = -pb.Phi[i, j] * Hi
+            rows.append(A); Ws.append(Rw[i]); rs.append(Y[b, i] - hi)
+        if pb.Pw is not None:  # prior, nlp/nlp.py:279-286
+            A = np.zeros((n, d)); A[:, :n] = np.eye(n)
+            rows.append(A); Ws.append(pb.Pw); rs.append(X[b, 0] - x0[b])
+        H = np.zeros((d, d)); g = np.zeros(d); c = 0.0
+        for A, Wm, r in zip(rows, Ws, rs):
+            H += A.T @ Wm @ A
+            g += A.T @ (Wm @ r)
+            c += r @ Wm @ r
+        Hs.append(H); gs.append(g); cs.append(c)
+    return np.stack(Hs), np.stack(gs), np.array(cs)
+
+
+def gauss_newton(pb, X0, U, Y, PAR=None, x0=None, max_iter=20, tol=1e-10):
+    """Batched GN with the same stopping rule as the HIP kernel.
+
+    Per trajectory: solve H delta = -g (Cholesky), X += delta, iters += 1;
+    converged when max|delta| <= tol * (1 + max|X|). Converged trajectories are
+    frozen. Returns X, cost (at the returned X), iters, status.
+    """
+    X = np.array(X0, dtype=np.float64, copy=True)
+    B = X.shape[0]
+    iters = np.zeros(B, dtype=np.int32)
+    status = np.full(B, MAXITER, dtype=np.int32)
+    active = np.ones(B, dtype=bool)
+    for _ in range(max_iter):
+        idx = np.nonzero(active)[0]
+        if idx.size == 0:
+            break
+        sub = lambda A: None if A is None else (A[idx] if A.shape[0] == B else A)
+        pbs = pb
+        if pb.Rw.ndim == 4:
+            pbs = _with_rw(pb, pb.Rw[idx])
+        H, g, _ = normal_equations(pbs, X[idx], sub(U), Y[idx], sub(PAR), sub(x0))
+        for t, b in enumerate(idx):
+            try:
+                L = np.linalg.cholesky(H[t])
+            except np.linalg.LinAlgError:
+                status[b] = NOT_SPD
+                active[b] = False
+                continue
+            delta = -np.linalg.solve(L.T, np.linalg.solve(L, g[t]))
+            if not np.all(np.isfinite(delta)):
+                status[b] = NONFINITE
+                active[b] = False
+                continue
+            X[b] += delta.reshape(X.shape[1:])
+            iters[b] += 1
+            if np.max(np.abs(delta)) <= tol * (1.0 + np.max(np.abs(X[b]))):
+                status[b] = OK
+                active[b] = False
+    _, _, _, cost = residuals(pb, X, U, Y, PAR, x0)
+    return X, cost, iters, status
+
+
+def gn_step_batched(pb, X, U, Y, PAR=None, x0=None):
+    """One vectorised GN iteration over the whole batch (CPU-baseline workload)."""
+    H, g, cost = normal_equations(pb, X, U, Y, PAR, x0)
+    L = np.linalg.cholesky(H)
+    z = np.linalg.solve(L, -g[..., None])
+    delta = np.linalg.solve(np.swapaxes(L, -1, -2), z)[..., 0]
+    return X + delta.reshape(X.shape), cost
+
+
+def _with_rw(pb, Rw):
+    q = Problem.__new__(Problem)
+    q.__dict__.update(pb.__dict__)
+    q.Rw = Rw
+    return q

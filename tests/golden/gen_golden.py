@@ -1,0 +1,268 @@
+"""Generate golden vectors from the reference implementation (build container only).
+
+Run:  python tests/golden/gen_golden.py   (needs /root/reference; writes tests/golden/*.npz)
+
+What it does
+  * imports the reference's own ``nlp/collocation.py``, ``nlp/dynamics.py``,
+    ``nlp/measurements.py``, ``nlp/cost_functions.py`` with a tiny numpy-backed
+    stand-in for the ``casadi`` *operators* they use (vertcat, sin, cos, tan,
+    sqrt, atan2, dot, norm_2, mtimes) -- CasADi itself is absent and the
+    plug-ins are plain expressions over those operators;
+  * ``collocation.py`` is Python-2 code: its ``range((N-a)/2 + 1)`` call gets a
+    module-global ``range`` that floors float bounds (Py-2 integer division), so
+    the reference's own ``__init__`` runs unmodified;
+  * imports ``utils/ekf.py`` and ``utils/gnss.py`` (flat imports, as the survey
+    documents) and runs the reference EKF on the gnss_stationary log;
+  * stores ONLY numbers (inputs and outputs) -- no reference source or bytecode
+    is written into this repository.
+
+The fixtures are consumed by ``tests/test_oracle_golden.py`` (oracle pinning)
+and by the GPU parity tests (``tests/test_gpu_*.py``).
+"""
+import builtins
+import importlib.util
+import os
+import sys
+import types
+
+import numpy as np
+
+REF = "/root/reference"
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+def _stub_casadi():
+    m = types.ModuleType("casadi")
+
+    def vertcat(*args):
+        parts = [np.atleast_1d(np.asarray(a)).ravel() for a in args]
+        return np.concatenate(parts)
+
+    m.vertcat = vertcat
+    m.sin, m.cos, m.tan, m.sqrt = np.sin, np.cos, np.tan, np.sqrt
+    m.atan2 = np.arctan2
+    m.dot = lambda a, b: np.sum(np.asarray(a) * np.asarray(b))
+    m.norm_2 = lambda a: np.sqrt(np.sum(np.asarray(a) ** 2))
+
+    def mtimes(a, b):
+        a = np.asarray(a)
+        b = np.asarray(b)
+        if a.ndim == 0 or b.ndim == 0:
+            return a * b
+        return a @ b
+
+    m.mtimes = mtimes
+    m.__all__ = []  # collocation.py does `from casadi import *` and uses nothing
+    return m
+
+
+def _load(name, path, extra_globals=None):
+    spec = importlib.util.spec_from_file_location(name, path)
+    mod = importlib.util.module_from_spec(spec)
+    if extra_globals:
+        mod.__dict__.update(extra_globals)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def _py2_range(*args):
+    return builtins.range(*[int(np.floor(a)) for a in args])
+
+
+def load_reference():
+    sys.modules.setdefault("casadi", _stub_casadi())
+    if "matplotlib.pyplot" not in sys.modules:
+        plt = types.ModuleType("matplotlib.pyplot")
+        mpl = types.ModuleType("matplotlib")
+        mpl.pyplot = plt
+        sys.modules["matplotlib"] = mpl
+        sys.modules["matplotlib.pyplot"] = plt
+    ref = types.SimpleNamespace()
+    ref.collocation = _load("ref_collocation", f"{REF}/nlp/collocation.py", {"range": _py2_range})
+    ref.dynamics = _load("ref_dynamics", f"{REF}/nlp/dynamics.py")
+    ref.measurements = _load("ref_measurements", f"{REF}/nlp/measurements.py")
+    ref.cost_functions = _load("ref_cost_functions", f"{REF}/nlp/cost_functions.py")
+    sys.path.insert(0, f"{REF}/utils")
+    try:
+        ref.ekf = _load("ref_ekf", f"{REF}/utils/ekf.py")
+        ref.gnss = _load("ref_gnss", f"{REF}/utils/gnss.py")
+        ref.gutils = _load("ref_gutils", f"{REF}/utils/utils.py")
+        ref.data = _load("ref_data", f"{REF}/utils/data.py")
+    finally:
+        sys.path.pop(0)
+    return ref
+
+
+def cstep_jac(fun, x, *rest, h=1e-30):
+    """Complex-step Jacobian of a plug-in at x (works through the stub operators)."""
+    x = np.asarray(x, dtype=np.float64)
+    f0 = np.atleast_1d(np.real(fun(x.astype(np.complex128), *rest)))
+    J = np.zeros((f0.shape[0], x.shape[0]))
+    for a in range(x.shape[0]):
+        xc = x.astype(np.complex128)
+        xc[a] += 1j * h
+        J[:, a] = np.imag(np.atleast_1d(fun(xc, *rest))) / h
+    return f0, J
+
+
+def cdiff_jac(fun, x, *rest, h=1e-6):
+    x = np.asarray(x, dtype=np.float64)
+    f0 = np.atleast_1d(fun(x, *rest)).astype(np.float64)
+    J = np.zeros((f0.shape[0], x.shape[0]))
+    for a in range(x.shape[0]):
+        xp = x.copy(); xp[a] += h
+        xm = x.copy(); xm[a] -= h
+        J[:, a] = (np.atleast_1d(fun(xp, *rest)) - np.atleast_1d(fun(xm, *rest))) / (2 * h)
+    return f0, J
+
+
+def gen_collocation(ref):
+    out = {}
+    for N in (2, 3, 4, 5, 6, 7, 10, 15, 20, 50, 100, 200, 500):
+        cpm = ref.collocation.ChebyshevPseudospectralMethod(N, 0, 10.0)
+        out[f"tau_{N}"] = np.asarray(cpm.tau)
+        D = np.ascontiguousarray(np.asarray(cpm.D, dtype=np.float64))
+        if N <= 100:
+            out[f"D_{N}"] = D
+        else:  # large N: sha256 of the bytes + probe entries keep the fixture small
+            import hashlib
+            out[f"Dsha_{N}"] = np.frombuffer(hashlib.sha256(D.tobytes()).digest(), dtype=np.uint8)
+            pr = np.random.default_rng(N).integers(0, N + 1, size=(256, 2))
+            out[f"Dprobe_idx_{N}"] = pr
+            out[f"Dprobe_val_{N}"] = D[pr[:, 0], pr[:, 1]]
+            out[f"Ddiag_{N}"] = np.diag(D).copy()
+        out[f"w_{N}"] = np.asarray(cpm.w)
+        if N <= 20:
+            ts = np.linspace(0.0, 10.0, 37)
+            out[f"phi_t_{N}"] = ts
+            out[f"phi_{N}"] = np.stack([cpm.evaluateLagrangePolynomials(t) for t in ts])
+            X = [np.array([np.sin(k), np.cos(2 * k)]) for k in range(N + 1)]
+            out[f"X_{N}"] = np.stack(X)
+            out[f"xeval_{N}"] = np.stack([cpm.evaluateSolution(t, X) for t in ts])
+    np.savez_compressed(os.path.join(OUT, "collocation.npz"), **out)
+
+
+DYN_CASES = {
+    # name: (n, m, params)
+    "single_integrator": (1, 1, None),
+    "single_integrator_2D": (2, 2, None),
+    "single_integrator_3D": (3, 3, None),
+    "double_integrator": (4, 2, None),
+    "van_der_pol": (2, 1, None),
+    "gnss_pos_and_bias": (5, 3, None),
+    "gnss_two_receiver": (10, 6, None),
+    "kinematic_bycicle_and_bias": (6, 2, None),
+}
+
+
+def gen_plugins(ref):
+    rng = np.random.default_rng(1234)
+    out = {}
+    for name, (n, m, params) in DYN_CASES.items():
+        f = getattr(ref.dynamics, name)
+        xs = rng.normal(size=(64, n))
+        us = rng.normal(size=(64, m))
+        fs, Fs = [], []
+        for x, u in zip(xs, us):
+            f0, J = cstep_jac(lambda xx, uu: f(xx, uu, params), x, u)
+            fs.append(f0)
+            Fs.append(J)
+        out[f"dyn_{name}_x"] = xs
+        out[f"dyn_{name}_u"] = us
+        out[f"dyn_{name}_f"] = np.stack(fs)
+        out[f"dyn_{name}_F"] = np.stack(Fs)
+    # m = 0 dynamics: f(x, params) (nlp/nlp.py:218)
+    xs = rng.normal(size=(64, 8))
+    fs, Fs = [], []
+    for x in xs:
+        f0, J = cstep_jac(lambda xx: ref.dynamics.multi_receiver(xx, None), x)
+        fs.append(f0); Fs.append(J)
+    out["dyn_multi_receiver_x"] = xs
+    out["dyn_multi_receiver_f"] = np.stack(fs)
+    out["dyn_multi_receiver_F"] = np.stack(Fs)
+
+    # measurements
+    def meas(name, n, mk_params, jac=cstep_jac):
+        h = getattr(ref.measurements, name)
+        xs = rng.normal(size=(64, n)) * 10.0
+        ys, Hs, pars = [], [], []
+        for x in xs:
+            p = mk_params()
+            y0, J = jac(lambda xx: h(xx, p), x)
+            ys.append(y0); Hs.append(J); pars.append(np.concatenate([np.ravel(v) for v in p.values()]) if p else np.zeros(0))
+        return xs, np.stack(ys), np.stack(Hs), np.stack(pars)
+
+    cases = {
+        "full_state": (3, lambda: None, cstep_jac),
+        "pseudorange": (5, lambda: {"sat_pos": rng.normal(size=3) * 2e4}, cstep_jac),
+        "vehicle_pseudorange": (9, lambda: {"sat_pos": rng.normal(size=3) * 2e4}, cstep_jac),
+        "pseudorange_rate": (8, lambda: {"sat_pos": rng.normal(size=3) * 2e4, "sat_vel": rng.normal(size=3) * 3e3}, cstep_jac),
+        "multi_receiver_range_3d": (10, lambda: {"y": rng.normal(size=3) * 10}, cstep_jac),
+        "multi_receiver_range_2d": (4, lambda: {"y": rng.normal(size=2) * 10}, cstep_jac),
+        "multi_receiver_heading_2d": (4, lambda: {"y": rng.normal(size=2) * 10}, cdiff_jac),
+    }
+    for name, (n, mk, jac) in cases.items():
+        xs, ys, Hs, pars = meas(name, n, mk, jac)
+        out[f"meas_{name}_x"] = xs
+        out[f"meas_{name}_y"] = ys
+        out[f"meas_{name}_H"] = Hs
+        out[f"meas_{name}_par"] = pars
+    # idx-variant of multi_receiver_range_3d used between receivers (gnss-multi-receiver.py)
+    h = ref.measurements.multi_receiver_range_3d
+    xs = rng.normal(size=(64, 10)) * 10.0
+    ys, Hs = [], []
+    for x in xs:
+        y0, J = cstep_jac(lambda xx: h(xx, {"idxA": [0, 1, 2], "idxB": [5, 6, 7]}), x)
+        ys.append(y0); Hs.append(J)
+    out["meas_range3d_AB_x"] = xs
+    out["meas_range3d_AB_y"] = np.stack(ys)
+    out["meas_range3d_AB_H"] = np.stack(Hs)
+
+    # cost functions (nlp/cost_functions.py)
+    vs = rng.normal(size=(16, 3))
+    Q = np.diag([2.0, 3.0, 0.5]) + 0.1
+    out["cost_v"] = vs
+    out["cost_Q"] = Q
+    out["cost_weighted_l2"] = np.array([float(np.squeeze(ref.cost_functions.weighted_l2_norm(v, {"Q": Q}))) for v in vs])
+    out["cost_l2"] = np.array([float(np.squeeze(ref.cost_functions.l2_norm(v))) for v in vs])
+    out["cost_huber"] = np.array([float(np.squeeze(ref.cost_functions.pseudo_huber_loss(v, {"Q": Q, "delta": 0.7}))) for v in vs])
+    np.savez_compressed(os.path.join(OUT, "plugins.npz"), **out)
+
+
+def gen_ekf(ref):
+    """Reference EKF on the gnss_stationary log (gnss_stationary.py:71-98 recipe)."""
+    data_path = f"{REF}/data/gnss_stationary/gnss_log_2020_02_05_09_14_15"
+    lat0, lon0, h0 = 37.4276, -122.1670, 0
+    p_ref = ref.gutils.lla2ecef(np.array([lat0, lon0, h0]))
+    data = ref.data.load_gnss_logs(data_path)
+    T = 50
+    Q = np.diag([0.0001, 0.0001, 0.0001, 0.1, 0.001])
+    r_pr = 100
+    u = np.zeros((3, T + 1))
+    mu0 = np.array([10.0, -5.0, 3.0, float(data["pr"][0][0]) * 0.0 + 1.0, 0.5])
+    S0 = np.eye(5)
+    filt = ref.ekf.EKF(ref.gnss.gnss_pos_and_bias, ref.gnss.multi_pseudorange, mu0.copy(), S0.copy())
+    mus, Ss, sats, prs, nsat = [], [], [], [], []
+    for k in range(T + 1):
+        sat_k = np.stack([ref.gutils.ecef2enu(data["sat_pos"][k][i, :], p_ref) for i in range(data["sat_pos"][k].shape[0])])
+        R = np.diag(r_pr * np.ones(data["pr"][k].shape[0]))
+        filt.update(u[:, k], data["pr"][k], Q, R, dyn_func_params={"dt": 1}, meas_func_params={"sat_pos": sat_k})
+        pad_s = np.zeros((12, 3)); pad_s[: sat_k.shape[0]] = sat_k
+        pad_p = np.zeros(12); pad_p[: sat_k.shape[0]] = data["pr"][k]
+        sats.append(pad_s); prs.append(pad_p); nsat.append(sat_k.shape[0])
+        mus.append(np.array(filt.mu, dtype=np.float64).copy()); Ss.append(np.array(filt.S).copy())
+    np.savez_compressed(os.path.join(OUT, "ekf_gnss_stationary.npz"), mu0=mu0, S0=S0, Q=Q, r_pr=np.array(r_pr, dtype=np.float64),
+                        sat_pos=np.stack(sats), pr=np.stack(prs), nsat=np.array(nsat, dtype=np.int32),
+                        mu=np.stack(mus), S=np.stack(Ss), dt=np.array(1.0))
+
+
+def main():
+    ref = load_reference()
+    gen_collocation(ref)
+    gen_plugins(ref)
+    gen_ekf(ref)
+    print("golden fixtures written to", OUT)
+
+
+if __name__ == "__main__":
+    main()

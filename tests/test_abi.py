@@ -1,0 +1,39 @@
+"""The C-ABI library loads and exports every symbol include/mhe.h declares (no GPU calls)."""
+import ctypes
+import os
+import re
+
+from mhe import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared():
+    src = open(os.path.join(ROOT, "include", "mhe.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(mhe_[a-z_]+)\s*\(", src)))
+
+
+def test_header_symbols_exported():
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    declared = _declared()
+    assert "mhe_gn_solve" in declared and "mhe_build_constants" in declared
+    for name in declared:
+        assert hasattr(lib, name), f"{name} declared in mhe.h but not exported"
+    assert set(declared) == set(_lib.SIGNATURES), "ctypes signature table out of sync with mhe.h"
+
+
+def test_host_side_entry_points_without_gpu():
+    lib = _lib.load()
+    assert lib.mhe_version().startswith(b"libmhe")
+    d = _lib.MheDims()
+    d.N, d.n, d.m, d.p, d.M, d.q, d.dyn_model, d.meas_model, d.T = 100, 2, 1, 2, 101, 0, 5, 1, 10.0
+    assert lib.mhe_padded_dim(d) == 208
+    assert lib.mhe_const_bytes(d) > 0
+    d.n = 3  # inconsistent with van der Pol
+    assert lib.mhe_const_bytes(d) == 0
+    assert lib.mhe_padded_dim(d) == -1
+    d.n, d.dyn_model = 2, 99
+    assert lib.mhe_const_bytes(d) == 0
+    d.dyn_model, d.N = 5, 500  # beyond the register-resident limit of this build
+    assert lib.mhe_padded_dim(d) == -1

@@ -1,0 +1,159 @@
+"""HIP path (through the C-ABI) vs the CPU oracle on identical seeded inputs.
+
+Tolerances (fp64 throughout):
+  assembly  H, g, cost     <= 1e-12 relative to max|.|   (same formulas, different summation order),
+                              times kappa = max|y| / max|y - h(x)|: pseudoranges (~2.2e7 m) with
+                              ~10 m residuals lose log10(kappa) digits to cancellation in y - h
+                              in ANY evaluation order (kappa = 1 when there is no cancellation)
+  dense SPD solve          <= 1e-10 relative              (cond(H) ~ 1e5 for C2)
+  Gauss-Newton iterate     <= 1e-9 * (1 + max|X|) after the same number of iterations
+  index / status / iteration counts: exact
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+from mhe import configs, solver  # noqa: E402
+from oracle import gn  # noqa: E402
+
+
+def _problem(w):
+    return gn.Problem(w.N, w.T, w.n, w.m, w.dyn, w.meas, w.cpm.D, (w.T / 2) * w.cpm.w,
+                      w.cpm.lagrange_matrix(w.t_meas), w.Qw, w.Rw, Pw=w.Pw, meas_static=w.meas_static)
+
+
+def _U(w):
+    return np.broadcast_to(w.U, (w.B,) + w.U.shape[1:])
+
+
+def _PAR(w):
+    return None if w.PAR is None else np.broadcast_to(w.PAR, (w.B,) + w.PAR.shape[1:])
+
+
+WORKLOADS = {
+    "c1": lambda: configs.make_c1(),
+    "c2_n20": lambda: configs.make_c2(B=6, N=20),
+    "c2_n100": lambda: configs.make_c2(B=6, N=100),
+    "gnss_small": lambda: configs.make_gnss_small(B=4),
+}
+
+
+@pytest.fixture(scope="module", params=sorted(WORKLOADS))
+def case(request):
+    w = WORKLOADS[request.param]()
+    return w, solver.from_workload(w), _problem(w)
+
+
+def _kappa(w, pb, X):
+    _, _, e, _ = gn.residuals(pb, X, _U(w), w.Y, _PAR(w))
+    return max(1.0, np.abs(w.Y).max() / np.abs(e).max())
+
+
+def test_assemble_matches_oracle(case):
+    w, s, pb = case
+    H, g, cost = s.assemble(w.X_init, w.U, w.Y, w.PAR)
+    H, g, cost = H.cpu().numpy(), g.cpu().numpy(), cost.cpu().numpy()
+    Hr, gr, cr = gn.normal_equations(pb, w.X_init, _U(w), w.Y, _PAR(w))
+    d = pb.d
+    k = _kappa(w, pb, w.X_init)
+    assert np.abs(H[:, :d, :d] - Hr).max() <= 1e-12 * np.abs(Hr).max()
+    assert np.abs(g[:, :d] - gr).max() <= 1e-12 * k * np.abs(gr).max()
+    assert np.allclose(cost, cr, rtol=1e-12 * k)
+    # padding: identity block, zero coupling, zero gradient
+    if s.dp > d:
+        assert np.array_equal(H[:, d:, d:], np.broadcast_to(np.eye(s.dp - d), H[:, d:, d:].shape))
+        assert not H[:, :d, d:].any() and not H[:, d:, :d].any() and not g[:, d:].any()
+
+
+def test_chol_solve_matches_numpy(case):
+    w, s, pb = case
+    rng = np.random.default_rng(7)
+    B, dp = 5, s.dp
+    A = rng.normal(size=(B, dp, dp))
+    H = A @ np.swapaxes(A, 1, 2) + dp * np.eye(dp)[None]
+    g = rng.normal(size=(B, dp))
+    delta, status = s.chol_solve(H, g)
+    ref = -np.linalg.solve(H, g[..., None])[..., 0]
+    assert np.all(status.cpu().numpy() == 0)
+    assert np.abs(delta.cpu().numpy() - ref).max() <= 1e-10 * np.abs(ref).max()
+
+
+def test_chol_solve_detects_non_spd(case):
+    w, s, pb = case
+    dp = s.dp
+    H = np.stack([np.eye(dp), np.eye(dp), np.eye(dp)])
+    H[1, dp // 2, dp // 2] = -1.0     # negative pivot
+    H[2, 3, 3] = np.nan               # non-finite pivot
+    delta, status = s.chol_solve(H, np.ones((3, dp)))
+    assert status.cpu().numpy().tolist() == [0, 2, 2]
+    assert np.allclose(delta.cpu().numpy()[0], -1.0)
+
+
+def test_gn_iterates_match_oracle(case):
+    w, s, pb = case
+    it = 4
+    X, cost, iters, status = s.solve(w.X_init, w.U, w.Y, w.PAR, max_iter=it, tol=0.0)
+    Xr, cr, ir, sr = gn.gauss_newton(pb, w.X_init, _U(w), w.Y, _PAR(w), max_iter=it, tol=0.0)
+    assert iters.cpu().numpy().tolist() == ir.tolist() == [it] * w.B
+    assert status.cpu().numpy().tolist() == sr.tolist() == [1] * w.B
+    X = X.cpu().numpy()
+    k = _kappa(w, pb, Xr)
+    assert np.abs(X - Xr).max() <= 1e-9 * k * (1 + np.abs(Xr).max())
+    assert np.allclose(cost.cpu().numpy(), cr, rtol=1e-9 * k)
+
+
+def test_gn_converges_to_oracle_optimum(case):
+    w, s, pb = case
+    X, cost, iters, status = s.solve(w.X_init, w.U, w.Y, w.PAR, max_iter=50, tol=1e-9)
+    Xr, cr, ir, sr = gn.gauss_newton(pb, w.X_init, _U(w), w.Y, _PAR(w), max_iter=50, tol=1e-9)
+    assert status.cpu().numpy().tolist() == sr.tolist() == [0] * w.B
+    assert np.all(np.abs(iters.cpu().numpy() - ir) <= 1)
+    k = _kappa(w, pb, Xr)
+    assert np.abs(X.cpu().numpy() - Xr).max() <= 1e-8 * k * (1 + np.abs(Xr).max())
+    assert np.allclose(cost.cpu().numpy(), cr, rtol=1e-10 * k)
+
+
+def test_max_iter_zero_returns_initial_iterate():
+    w = configs.make_c2(B=3, N=20)
+    s = solver.from_workload(w)
+    X, cost, iters, status = s.solve(w.X_init, w.U, w.Y, max_iter=0)
+    assert np.array_equal(X.cpu().numpy(), w.X_init)
+    assert iters.cpu().numpy().tolist() == [0, 0, 0]
+    _, _, _, cr = gn.residuals(_problem(w), w.X_init, _U(w), w.Y)
+    assert np.allclose(cost.cpu().numpy(), cr, rtol=1e-12)
+
+
+def test_empty_batch_is_noop():
+    w = configs.make_c2(B=1, N=20)
+    s = solver.from_workload(w)
+    X, cost, iters, status = s.solve(np.zeros((0, w.P, w.n)), w.U, np.zeros((0, w.M, w.p)), max_iter=3)
+    assert X.shape == (0, w.P, w.n)
+
+
+def test_nonfinite_input_is_reported_not_fatal():
+    w = configs.make_c2(B=3, N=20)
+    s = solver.from_workload(w)
+    X0 = w.X_init.copy()
+    X0[1, 5, 0] = np.nan
+    X, cost, iters, status = s.solve(X0, w.U, w.Y, max_iter=40, tol=1e-9)
+    st = status.cpu().numpy().tolist()
+    assert st[0] == 0 and st[2] == 0 and st[1] in (2, 3)
+
+
+def test_c2_full_batch_properties():
+    """BASELINE configs[1] at full size (B=1024, N=100): every trajectory converges,
+    the cost drops, and a subset matches the oracle."""
+    w = configs.make_c2(B=1024)
+    s = solver.from_workload(w)
+    X, cost, iters, status = s.solve(w.X_init, w.U, w.Y, max_iter=30, tol=1e-9)
+    st = status.cpu().numpy()
+    assert (st == 0).all()
+    pb = _problem(w)
+    _, _, _, c0 = gn.residuals(pb, w.X_init, _U(w), w.Y)
+    assert (cost.cpu().numpy() < c0).all()
+    sub = np.arange(0, 1024, 128)
+    Xr, cr, ir, sr = gn.gauss_newton(pb, w.X_init[sub], _U(w)[sub], w.Y[sub], max_iter=30, tol=1e-9)
+    assert np.abs(X.cpu().numpy()[sub] - Xr).max() <= 1e-8 * (1 + np.abs(Xr).max())

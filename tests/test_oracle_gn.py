@@ -1,0 +1,69 @@
+"""The GN oracle itself: structured vs explicit normal equations, and the GN
+optimum vs an independent optimiser (scipy least_squares on the same objective)."""
+import numpy as np
+import pytest
+from scipy.optimize import least_squares
+
+from mhe import configs
+from oracle import gn
+
+
+def _problem(w):
+    return gn.Problem(w.N, w.T, w.n, w.m, w.dyn, w.meas, w.cpm.D, (w.T / 2) * w.cpm.w,
+                      w.cpm.lagrange_matrix(w.t_meas), w.Qw, w.Rw, Pw=w.Pw, meas_static=w.meas_static)
+
+
+@pytest.mark.parametrize("make,kw", [(configs.make_c1, {}), (configs.make_c2, {"B": 2, "N": 20})])
+def test_structured_equals_explicit(make, kw):
+    w = make(**kw)
+    pb = _problem(w)
+    U = np.broadcast_to(w.U, (w.B,) + w.U.shape[1:])
+    H1, g1, c1 = gn.normal_equations(pb, w.X_init, U, w.Y)
+    H2, g2, c2 = gn.normal_equations_explicit(pb, w.X_init, U, w.Y)
+    assert np.abs(H1 - H2).max() <= 1e-13 * np.abs(H2).max()
+    assert np.abs(g1 - g2).max() <= 1e-12 * np.abs(g2).max()
+    assert np.allclose(c1, c2, rtol=1e-13)
+
+
+def test_gn_optimum_matches_least_squares():
+    w = configs.make_c2(B=1, N=30)
+    pb = _problem(w)
+    U = np.broadcast_to(w.U, (1,) + w.U.shape[1:])
+    X, cost, iters, status = gn.gauss_newton(pb, w.X_init, U, w.Y, max_iter=40, tol=1e-13)
+    assert status[0] == gn.OK
+
+    def resid(xf):
+        Wd, _, e, _ = gn.residuals(pb, xf.reshape(1, w.P, w.n), U, w.Y)
+        rd = (np.sqrt(pb.c)[:, None] * Wd[0] * np.sqrt(np.diag(pb.Qw))[None, :]).ravel()
+        rm = (e[0] * np.sqrt(np.array([np.diag(r) for r in pb.Rw]))).ravel()
+        return np.concatenate([rd, rm])
+
+    sol = least_squares(resid, w.X_init[0].ravel(), jac="3-point", xtol=1e-15, ftol=1e-15, gtol=1e-15,
+                        method="lm")
+    # LM with a finite-difference Jacobian terminates on its own ftol: loose
+    assert np.abs(sol.x.reshape(w.P, w.n) - X[0]).max() <= 2e-6 * (1 + np.abs(X[0]).max())
+    assert abs(2 * sol.cost - cost[0]) <= 1e-10 * cost[0]
+    assert 2 * sol.cost >= cost[0] * (1 - 1e-14)  # GN is at least as good
+
+
+def test_gn_optimum_is_stationary_fd():
+    """Independent of every Jacobian formula: central-difference gradient of the
+    reference objective at the GN optimum is ~0 (relative to the initial gradient)."""
+    w = configs.make_c2(B=1, N=20)
+    pb = _problem(w)
+    U = np.broadcast_to(w.U, (1,) + w.U.shape[1:])
+    X, cost, iters, status = gn.gauss_newton(pb, w.X_init, U, w.Y, max_iter=40, tol=1e-13)
+
+    def J(x):
+        return gn.residuals(pb, x.reshape(1, w.P, w.n), U, w.Y)[3][0]
+
+    def fd_grad(x, h=1e-6):
+        g = np.zeros_like(x)
+        for i in range(x.size):
+            e = np.zeros_like(x); e[i] = h
+            g[i] = (J(x + e) - J(x - e)) / (2 * h)
+        return g
+
+    g0 = fd_grad(w.X_init[0].ravel())
+    gs = fd_grad(X[0].ravel())
+    assert np.abs(gs).max() <= 1e-6 * np.abs(g0).max()
