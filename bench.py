@@ -1,0 +1,186 @@
+"""Benchmark: Gauss-Newton collocation-point updates/sec (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1]): van der Pol (nlp/dynamics.py:61-66),
+full_state measurements, N=100 (P=101 CGL nodes), T=10, M=101, batch 1024
+independent trajectories per GPU (weak scaling: each rank solves its own
+seeded shard; the only collectives are the one-time RCCL broadcast of the
+model constants and the max-over-ranks of the elapsed time).
+
+One step = one mhe_gn_solve launch over the resident batch doing exactly
+GN_ITERS full Gauss-Newton iterations per trajectory (tol = 0): residual +
+Jacobian, J^T W J / J^T W r assembly, register-tiled Cholesky, two triangular
+solves, update.  value = (all ranks) B * P * GN_ITERS * K / max-rank wall.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu]
+N > 1 is launched by torch.distributed.run (RANK/LOCAL_RANK/WORLD_SIZE env).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "nlp-filter_amd"))
+sys.path.insert(0, ROOT)
+
+GN_ITERS = 10
+FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 vector / matrix (spec); MI355X_MICROARCH.md lists no fp64 row
+HBM_PEAK_GBS = 8000.0
+
+
+def algorithmic_flops_per_traj_iter(P, n, M):
+    """FLOPs one GN iteration of one trajectory needs (d = P n):
+    Cholesky d^3/3, two triangular solves 2 d^2, X-dependent J^T W J terms
+    (6 flops per lower-triangle element), residual/gradient mat-vecs
+    (D X, D^T V, Phi X, Phi^T G e: 2 P^2 n + 2 P^2 n + 2 M P n + 2 M P n)."""
+    d = P * n
+    return d ** 3 / 3.0 + 2.0 * d * d + 6.0 * d * (d + 1) / 2.0 + 4.0 * P * P * n + 4.0 * M * P * n
+
+
+def algorithmic_bytes_per_traj(P, n, m, M, p):
+    """HBM bytes per trajectory per launch: X in, U, Y in, X out, cost/iters/status.
+    (Constants -- D, Phi, the constant J^T W J tiles -- are shared by every
+    workgroup and L2/MALL resident; they are not per-trajectory traffic.)"""
+    return 8.0 * (P * n + M * p + P * n) + 8 + 4 + 4
+
+
+def cpu_baseline(w, iters, sample_B):
+    """The oracle's CPU port of the same GN iteration on the host cores
+    (thread pool over trajectories, BLAS single-threaded inside each worker)."""
+    from concurrent.futures import ThreadPoolExecutor
+    from threadpoolctl import threadpool_limits
+    from oracle import gn
+
+    cores = len(os.sched_getaffinity(0))
+    cores = min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)))
+    pb = gn.Problem(w.N, w.T, w.n, w.m, w.dyn, w.meas, w.cpm.D, (w.T / 2) * w.cpm.w,
+                    w.cpm.lagrange_matrix(w.t_meas), w.Qw, w.Rw)
+    port = gn.CpuPort(pb)
+    B = min(sample_B, w.B)
+    U = np.broadcast_to(w.U, (B,) + w.U.shape[1:])
+    chunks = np.array_split(np.arange(B), cores)
+
+    def work(ix):
+        X = w.X_init[ix].copy()
+        for _ in range(iters):
+            X = port.iteration(X, U[ix], w.Y[ix])
+        return X
+
+    with threadpool_limits(1):
+        work(chunks[0][:2])  # warm-up
+        t0 = time.perf_counter()
+        with ThreadPoolExecutor(max_workers=cores) as ex:
+            list(ex.map(work, chunks))
+        dt = time.perf_counter() - t0
+    return {"value": B * w.P * iters / dt, "unit": "GN collocation-point updates/s", "cores": cores,
+            "kind": "port",
+            "sample": f"{B} of the {w.B} trajectories x {iters} GN iterations (oracle.gn.CpuPort, "
+                      f"{cores} worker threads, LAPACK dpotrf per trajectory), {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=1024, help="trajectories per GPU")
+    ap.add_argument("--iters", type=int, default=GN_ITERS)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-sample", type=int, default=512)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from mhe import configs, solver
+
+    w = configs.make_c2(B=args.batch, seed=1 + 1000 * rank)
+    s = solver.from_workload(w, device=dev)
+    if world > 1:
+        # model constants: built on rank 0, broadcast over RCCL/xGMI (one-time, untimed)
+        dist.broadcast(s.cbuf, src=0)
+    staged = s.prepare(w.X_init, w.U, w.Y)
+    B = args.batch
+    outs = (torch.empty_like(staged[0]), torch.empty(B, dtype=torch.float64, device=dev),
+            torch.empty(B, dtype=torch.int32, device=dev), torch.empty(B, dtype=torch.int32, device=dev))
+    stream = torch.cuda.current_stream(dev)
+
+    for _ in range(args.warmup):
+        s.solve_staged(staged, outs, args.iters, 0.0, stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        s.solve_staged(staged, outs, args.iters, 0.0, stream)
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    kern_ms = ev0.elapsed_time(ev1) / args.steps  # launches are back to back on `stream`
+
+    iters_done = outs[2].sum().item()
+    if world > 1:
+        t = torch.tensor([wall], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = t.item()
+        it = torch.tensor([iters_done], dtype=torch.float64, device=dev)
+        dist.all_reduce(it, op=dist.ReduceOp.SUM)
+        iters_done = it.item()
+    total_updates = iters_done * w.P * args.steps  # sum over ranks of B * P * iters per step
+    value = total_updates / wall
+
+    if rank == 0:
+        fl = algorithmic_flops_per_traj_iter(w.P, w.n, w.M) * B * args.iters
+        achieved = fl / (kern_ms * 1e-3) / 1e12
+        rec = {
+            "metric": "Gauss-Newton collocation-point updates/sec",
+            "value": value,
+            "unit": "GN collocation-point updates/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": wall / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (seeded van der Pol truth via RK4 + Gaussian noise, R/Q from estimation_example.py)",
+            "config": {"workload": "C2 van_der_pol: n=2, m=1, full_state p=2, N=100 (P=101, d=202), T=10, M=101",
+                       "global_batch": B * world, "batch_per_gpu": B, "gn_iters_per_step": args.iters,
+                       "parallelism": f"dp{world} (independent trajectories; RCCL broadcast of constants only)"},
+            "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None,
+                         "kernel": "k_gn<DynVanDerPol,MeasFullState<2>,23,0>",
+                         "kernel_ms": kern_ms,
+                         "flops_per_launch": fl,
+                         "hbm_algorithmic_GBs": algorithmic_bytes_per_traj(w.P, w.n, w.m, w.M, w.p) * B / (kern_ms * 1e-3) / 1e9},
+        }
+        if world == 1 and not args.no_cpu:
+            rec["cpu_baseline"] = cpu_baseline(w, args.iters, args.cpu_sample)
+        print(json.dumps(rec))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -187,3 +187,54 @@ def _with_rw(pb, Rw):
     q.__dict__.update(pb.__dict__)
     q.Rw = Rw
     return q
+
+
+# --------------------------------------------------------------------------
+# CPU port of the per-iteration algorithm (bench.py cpu_baseline leg).
+# Same split as the HIP kernel: the X-independent part of J^T W J (dynamics
+# a^2 (D^T C D) (x) Qw, linear-measurement information, prior) is built once;
+# every iteration adds the X-dependent dynamics terms, factors with batched
+# LAPACK Cholesky and does two triangular solves per trajectory.
+class CpuPort:
+    def __init__(self, pb):
+        if pb.meas != "full_state" or pb.Rw.ndim != 3:
+            raise NotImplementedError("CpuPort covers the linear-measurement configs (C1, C2)")
+        P, n, a = pb.P, pb.n, pb.alpha
+        DCD = np.einsum("kj,k,kl->jl", pb.D, pb.c, pb.D)
+        H4 = (a * a) * np.einsum("jl,ae->jale", DCD, pb.Qw)
+        PR = pb.Phi[:, :, None] * pb.Phi[:, None, :]                   # (M,P,P)
+        H4 += np.einsum("ijl,iae->jale", PR, pb.Rw)
+        if pb.Pw is not None:
+            H4[0, :, 0, :] += pb.Pw
+        self.pb = pb
+        self.Hc = H4.reshape(P * n, P * n)
+
+    def iteration(self, X, U, Y, x0=None):
+        """One GN iteration for the whole batch; returns X + delta."""
+        import scipy.linalg as sla
+        pb = self.pb
+        B, P, n = X.shape
+        d = P * n
+        W, xi, e, cost = residuals(pb, X, U, Y, None, x0)
+        _, F = models.dyn_eval(pb.dyn, X, U)
+        E = np.einsum("k,ac,zkce->zkae", pb.c, pb.Qw, F)
+        # M[(j,a),(l,e)] = D_lj E_l[a,e];  H = Hc - a (M + M^T) + blkdiag(F^T E)
+        Mx = (pb.D.T[None, :, None, :, None] * E.transpose(0, 2, 1, 3)[:, None]).reshape(B, d, d)
+        H = self.Hc[None] - pb.alpha * (Mx + np.swapaxes(Mx, 1, 2))
+        FtE = np.einsum("zjca,zjce->zjae", F, E)
+        for k in range(P):
+            H[:, k * n:(k + 1) * n, k * n:(k + 1) * n] += FtE[:, k]
+        V = np.einsum("k,ac,zkc->zka", pb.c, pb.Qw, W)
+        g = pb.alpha * np.einsum("kj,zka->zja", pb.D, V) - np.einsum("zjca,zjc->zja", F, V)
+        ge = np.einsum("ipq,ziq->zip", pb.Rw, e)
+        g -= np.einsum("ij,zia->zja", pb.Phi, ge)
+        if pb.Pw is not None:
+            g[:, 0] += (X[:, 0] - x0) @ pb.Pw.T
+        g = g.reshape(B, d)
+        L = np.linalg.cholesky(H)
+        out = np.empty_like(X)
+        for b in range(B):
+            y = sla.solve_triangular(L[b], -g[b], lower=True, check_finite=False)
+            delta = sla.solve_triangular(L[b], y, lower=True, trans="T", check_finite=False)
+            out[b] = X[b] + delta.reshape(P, n)
+        return out
