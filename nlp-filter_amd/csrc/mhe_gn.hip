@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "mhe.h"
 #include "mhe_models.h"
@@ -39,7 +40,7 @@ enum Mode { MODE_SOLVE = 0, MODE_ASSEMBLE = 1, MODE_LINSOLVE = 2 };
 
 // ------------------------------------------------------------ layouts
 struct ConstLayout {
-  size_t D, Dt, Phi, PhiT, cw, Qw, Pw, Rw, Cc, tab, total;  // byte offsets
+  size_t D, Dt, Phi, PhiT, cw, Qw, Pw, Rw, Cc, DA, DB, total;  // byte offsets
 };
 
 __host__ __device__ inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
@@ -56,14 +57,15 @@ __host__ __device__ inline ConstLayout const_layout(int P, int M, int n, int p, 
   L.Qw = o;   o = align256(o + sizeof(double) * n * n);
   L.Pw = o;   o = align256(o + sizeof(double) * n * n);
   L.Rw = o;   o = align256(o + sizeof(double) * M * p * p);
-  L.Cc = o;   o = align256(o + sizeof(double) * ntiles * 256);
-  L.tab = o;  o = align256(o + sizeof(int) * ntiles);
+  L.Cc = o;   o = align256(o + sizeof(double) * ntiles * 256);  // constant part of J^T W J
+  L.DA = o;   o = align256(o + sizeof(double) * ntiles * 256);  // a * D[l][j] per tile element
+  L.DB = o;   o = align256(o + sizeof(double) * ntiles * 256);  // a * D[j][l] per tile element
   L.total = o;
   return L;
 }
 
 struct SmemLayout {  // offsets in doubles
-  int Xs, Vs, FtV, Es, FtE, GE, G, BV, DV, IDG, PB0, PB1, PART, RED, TAB, total;
+  int Xs, Vs, FtV, Es, FtE, GE, G, BV, YV, IDG, PB0, PB1, LKK, PART, RED, total;
 };
 
 __host__ __device__ inline int rnd2(int x) { return (x + 1) & ~1; }  // keep 16-B alignment
@@ -79,14 +81,14 @@ __host__ __device__ inline SmemLayout smem_layout(int P, int M, int n, int NT, b
   S.FtE = o;  o += rnd2(P * n * n);
   S.GE = o;   o += rnd2(M * n);
   S.G = o;    o += nonlinear ? rnd2(M * n * n) : 0;
-  S.BV = o;   o += dp;
-  S.DV = o;   o += dp;
-  S.IDG = o;  o += dp;
-  S.PB0 = o;  o += dp * PBS;
+  S.BV = o;   o += dp;          // working right-hand side (panel sweeps update it row-wise)
+  S.YV = o;   o += dp;          // y = L^-1 (-g), then delta = L^-T y in place
+  S.IDG = o;  o += dp;          // 1 / L_cc
+  S.PB0 = o;  o += dp * PBS;    // panel buffers (double-buffered over steps)
   S.PB1 = o;  o += dp * PBS;
+  S.LKK = o;  o += 16 * PBS;    // factored diagonal block of the current step
   S.PART = o; o += NW * 16;
   S.RED = o;  o += 4 * NW + 8;
-  S.TAB = o;  o += (NW * MAX_SLOTS + 1) / 2 + 1;  // int tile table (I | J << 16), -1 = no tile
   S.total = o;
   return S;
 }
@@ -114,7 +116,24 @@ struct GnArgs {
   const double* Hin;
   const double* gin;
   double* dout;
+  unsigned long long* dbg;  // MHE_DIAG builds only: per-phase cycle sums
 };
+
+#ifdef MHE_DIAG
+// Diagnostic build: s_memtime stamps at phase boundaries (wave 0), summed per
+// workgroup.  Never compiled into the product library.
+#define DIAG_DECL unsigned long long _dg[16] = {}; unsigned long long _dt = __builtin_amdgcn_s_memtime();
+#define DIAG_MARK(i) do { const unsigned long long _n = __builtin_amdgcn_s_memtime(); _dg[i] += _n - _dt; _dt = _n; } while (0)
+#define DIAG_FLUSH(b) do { if (threadIdx.x == 0 && a.dbg) for (int _i = 0; _i < 16; ++_i) a.dbg[(b) * 16 + _i] = _dg[_i]; } while (0)
+#define DIAG_FDECL unsigned long long* _dg, unsigned long long& _dt
+#define DIAG_FARGS _dg, _dt
+#else
+#define DIAG_DECL
+#define DIAG_MARK(i) do { } while (0)
+#define DIAG_FLUSH(b) do { } while (0)
+#define DIAG_FDECL int
+#define DIAG_FARGS 0
+#endif
 
 // ------------------------------------------------------------ wave helpers
 __device__ __forceinline__ double readlane_d(double v, int lane) {
@@ -157,13 +176,65 @@ __device__ __forceinline__ void block_reduce2(double* red, double& a, double& b,
   b = rb;
 }
 
-// Tile coordinates of linear tile t (column-major lower triangle), read from
-// the LDS copy of the table and made wave-uniform.  Reading from LDS (rather
-// than the constants buffer) keeps the compiler from hoisting 23 slots' worth
-// of table values out of the step loops into SGPRs.
-__device__ __forceinline__ int tile_IJ(const int* tab, int t) { return __builtin_amdgcn_readfirstlane(tab[t]); }
+// Slot table: lane s of every wave holds (I | J << 16) of the tile in its slot
+// s (tile t = wave + NW*s, column-major over the lower triangle), -1 = none.
+// A slot's coordinates are one v_readlane away (no memory round trip); callers
+// pass an opaque per-step copy so LICM cannot hoist 23 decoded values.
+__device__ __forceinline__ int make_slot_table(int wave, int lane, int NT, int ntiles) {
+  const int t = wave + NW * lane;
+  if (lane >= MAX_SLOTS || t >= ntiles) return -1;
+  int J = 0, base = 0;
+  while (t >= base + (NT - J)) {
+    base += NT - J;
+    ++J;
+  }
+  return (J + (t - base)) | (J << 16);
+}
+
+__device__ __forceinline__ int slot_ij(int stab, int s) { return __builtin_amdgcn_readlane(stab, s); }
 
 // ------------------------------------------------------------ model phases
+// Mat-vec phases use TPR = 2 threads per row: each sums half of the row with
+// an 8-deep unrolled loop (8 independent L2 loads in flight), the halves are
+// combined with one lane swap.  The tables (D, D^T, Phi, Phi^T) are shared by
+// every workgroup and L2-resident.
+constexpr int TPR = 2;
+
+// threadIdx.x through an opaque move: values derived from it inside a phase
+// are recomputed per phase instead of being hoisted out of the Gauss-Newton
+// loop, where they would stay live across the register-hungry factorization.
+__device__ __forceinline__ int opaque_tid() {
+  int t = threadIdx.x;
+  asm volatile("" : "+v"(t));
+  return t;
+}
+
+template <int n>
+__device__ __forceinline__ void dot_rows_half(const double* __restrict__ Mt, int ld, int row, int len, int half,
+                                              const double* __restrict__ Xs, double (&acc)[n]) {
+  // acc[c] = sum_{j = half, half+2, ...} Mt[j*ld + row] * Xs[j*n + c]
+#pragma unroll
+  for (int c = 0; c < n; ++c) acc[c] = 0.0;
+  int j = half;
+#pragma unroll 1
+  for (; j + 2 * 7 < len; j += 2 * 8) {
+    double m[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) m[u] = Mt[(j + 2 * u) * ld + row];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+#pragma unroll
+      for (int c = 0; c < n; ++c) acc[c] += m[u] * Xs[(j + 2 * u) * n + c];
+  }
+  for (; j < len; j += 2) {
+    const double mv = Mt[j * ld + row];
+#pragma unroll
+    for (int c = 0; c < n; ++c) acc[c] += mv * Xs[j * n + c];
+  }
+#pragma unroll
+  for (int c = 0; c < n; ++c) acc[c] += __shfl_xor(acc[c], 1);
+}
+
 // Per-node dynamics quantities (nlp/nlp.py:225-245):
 //   W_k = a * sum_j D_kj X_j - f(X_k, U_k);  V_k = c_k Qw W_k;  E_k = c_k Qw F_k;
 //   FtE_k = F_k^T E_k;  FtV_k = F_k^T V_k;   cost += c_k W_k^T Qw W_k
@@ -175,15 +246,14 @@ __device__ __forceinline__ double node_phase(const GnArgs& a, const ConstLayout&
   const double* Qw = (const double*)(a.cbuf + CL.Qw);
   const double* Xs = sm + SL.Xs;
   double cost = 0.0;
-  for (int k = threadIdx.x; k < a.P; k += NTHREADS) {
+  const int tid = opaque_tid();
+  const int half = tid & 1;
+  for (int k0 = 0; k0 < a.P; k0 += NTHREADS / TPR) {
+    const int k = k0 + (tid >> 1);
+    const int kk = k < a.P ? k : a.P - 1;
     double dx[n];
-#pragma unroll
-    for (int c = 0; c < n; ++c) dx[c] = 0.0;
-    for (int j = 0; j < a.P; ++j) {
-      const double djk = Dt[j * a.P + k];
-#pragma unroll
-      for (int c = 0; c < n; ++c) dx[c] += djk * Xs[j * n + c];
-    }
+    dot_rows_half<n>(Dt, a.P, kk, a.P, half, Xs, dx);
+    if (half || k >= a.P) continue;
     double xk[n], uk[m > 0 ? m : 1], f[n], F[n * n];
 #pragma unroll
     for (int c = 0; c < n; ++c) xk[c] = Xs[k * n + c];
@@ -249,15 +319,14 @@ __device__ __forceinline__ double meas_phase(const GnArgs& a, const ConstLayout&
   const double* Rw = (const double*)(a.cbuf + CL.Rw);
   const double* Xs = sm + SL.Xs;
   double cost = 0.0;
-  for (int i = threadIdx.x; i < a.M; i += NTHREADS) {
+  const int tid = opaque_tid();
+  const int half = tid & 1;
+  for (int i0 = 0; i0 < a.M; i0 += NTHREADS / TPR) {
+    const int i = i0 + (tid >> 1);
+    const int ii = i < a.M ? i : a.M - 1;
     double xi[n];
-#pragma unroll
-    for (int c = 0; c < n; ++c) xi[c] = 0.0;
-    for (int j = 0; j < a.P; ++j) {
-      const double ph = PhiT[j * a.M + i];
-#pragma unroll
-      for (int c = 0; c < n; ++c) xi[c] += ph * Xs[j * n + c];
-    }
+    dot_rows_half<n>(PhiT, a.M, ii, a.P, half, Xs, xi);
+    if (half || i >= a.M) continue;
     double par[q > 0 ? q : 1];
     if (q > 0) {
       const double* PR = a.PAR + (long long)b * a.pstride + (long long)i * q;
@@ -313,7 +382,9 @@ __device__ __forceinline__ double meas_phase(const GnArgs& a, const ConstLayout&
   return cost;
 }
 
-// Gradient g = J^T W r; writes BV = -g (padding 0).  Also the prior cost.
+// Gradient g = J^T W r (nlp/nlp.py:242-286 objective); writes BV = -g (padding 0).
+//   g_j = a sum_k D_kj V_k - F_j^T V_j - sum_i Phi_ij GE_i (+ Pw (X_0 - x0) at j = 0)
+// Thread pair per node: even lane sums the D column, odd lane the Phi column.
 template <class DYN>
 __device__ __forceinline__ double grad_phase(const GnArgs& a, const ConstLayout& CL, const SmemLayout& SL, double* sm, int b) {
   constexpr int n = DYN::n;
@@ -327,39 +398,58 @@ __device__ __forceinline__ double grad_phase(const GnArgs& a, const ConstLayout&
   double* BV = sm + SL.BV;
   double cost = 0.0;
   const int dp = 16 * a.NT;
-  for (int j = threadIdx.x; j < a.P; j += NTHREADS) {
+  const int tid = opaque_tid();
+  const int odd = tid & 1;
+  for (int j0 = 0; j0 < a.P; j0 += NTHREADS / TPR) {
+    const int j = j0 + (tid >> 1);
+    const int jj = j < a.P ? j : a.P - 1;
+    // even lane: sum_k D[k][j] V_k ; odd lane: sum_i Phi[i][j] GE_i
+    const double* Mt = odd ? Phi : D;
+    const double* vec = odd ? GE : Vs;
+    const int len = odd ? a.M : a.P;
+    double s[n];
+#pragma unroll
+    for (int c = 0; c < n; ++c) s[c] = 0.0;
+    int k = 0;
+#pragma unroll 1
+    for (; k + 7 < len; k += 8) {
+      double mv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) mv[u] = Mt[(k + u) * a.P + jj];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+#pragma unroll
+        for (int c = 0; c < n; ++c) s[c] += mv[u] * vec[(k + u) * n + c];
+    }
+    for (; k < len; ++k) {
+      const double mv = Mt[k * a.P + jj];
+#pragma unroll
+      for (int c = 0; c < n; ++c) s[c] += mv * vec[k * n + c];
+    }
+    double o[n];
+#pragma unroll
+    for (int c = 0; c < n; ++c) o[c] = __shfl_xor(s[c], 1);
+    if (odd || j >= a.P) continue;
     double gv[n];
 #pragma unroll
-    for (int c = 0; c < n; ++c) gv[c] = 0.0;
-    for (int k = 0; k < a.P; ++k) {
-      const double dkj = D[k * a.P + j];
-#pragma unroll
-      for (int c = 0; c < n; ++c) gv[c] += dkj * Vs[k * n + c];
-    }
-#pragma unroll
-    for (int c = 0; c < n; ++c) gv[c] = a.alpha * gv[c] - FtV[j * n + c];
-    for (int i = 0; i < a.M; ++i) {
-      const double ph = Phi[i * a.P + j];
-#pragma unroll
-      for (int c = 0; c < n; ++c) gv[c] -= ph * GE[i * n + c];
-    }
+    for (int c = 0; c < n; ++c) gv[c] = a.alpha * s[c] - FtV[j * n + c] - o[c];
     if (a.has_prior && j == 0) {
       double r0[n];
 #pragma unroll
       for (int c = 0; c < n; ++c) r0[c] = Xs[c] - a.x0[(long long)b * n + c];
 #pragma unroll
       for (int r = 0; r < n; ++r) {
-        double s = 0.0;
+        double t2 = 0.0;
 #pragma unroll
-        for (int c = 0; c < n; ++c) s += Pw[r * n + c] * r0[c];
-        gv[r] += s;
-        cost += r0[r] * s;
+        for (int c = 0; c < n; ++c) t2 += Pw[r * n + c] * r0[c];
+        gv[r] += t2;
+        cost += r0[r] * t2;
       }
     }
 #pragma unroll
     for (int c = 0; c < n; ++c) BV[j * n + c] = -gv[c];
   }
-  for (int t = a.d + threadIdx.x; t < dp; t += NTHREADS) BV[t] = 0.0;
+  for (int t = a.d + tid; t < dp; t += NTHREADS) BV[t] = 0.0;
   return cost;
 }
 
@@ -367,39 +457,41 @@ __device__ __forceinline__ double grad_phase(const GnArgs& a, const ConstLayout&
 //   H = Cc (constant: a^2 (D^T C D) (x) Qw  + linear-measurement term + prior + padding I)
 //     - a D_lj E_l[a,b] - a D_jl E_j[b,a] + delta_jl (F^T E)_j[a,b]      (dynamics, X-dependent)
 //     + sum_i Phi_ij Phi_il G_i[a,b]                                      (nonlinear measurements)
+// Cc, DA = a D_lj and DB = a D_jl are stored per tile element in the MFMA
+// C-layout, so each is one coalesced 512-B load per register.
 template <class DYN, class MEAS, int SLOTS>
 __device__ __forceinline__ void build_tiles(const GnArgs& a, const ConstLayout& CL, const SmemLayout& SL, double* sm,
-                            d4 (&acc)[SLOTS], int wave, int lane) {
+                                            d4 (&acc)[SLOTS], int wave, int lane, int stab) {
   constexpr int n = DYN::n;
   const double* Cc = (const double*)(a.cbuf + CL.Cc);
-  const double* D = (const double*)(a.cbuf + CL.D);
+  const double* DA = (const double*)(a.cbuf + CL.DA);
+  const double* DB = (const double*)(a.cbuf + CL.DB);
   const double* Phi = (const double*)(a.cbuf + CL.Phi);
-  const int* tab = (const int*)(sm + SL.TAB);
   const double* Es = sm + SL.Es;
   const double* FtE = sm + SL.FtE;
   const double* G = sm + SL.G;
-  // opaque copies: the per-slot tile pointers would otherwise be hoisted out
-  // of the Gauss-Newton loop (23 live 64-bit addresses -> spills)
   asm volatile("" : "+v"(lane));
   asm volatile("" : "+s"(wave));
+  asm volatile("" : "+v"(stab));
 #pragma unroll
   for (int s = 0; s < SLOTS; ++s) {
-    const int t = wave + NW * s;
-    const int IJ = tile_IJ(tab, t);
+    const int IJ = slot_ij(stab, s);
     if (IJ < 0) {
       acc[s] = d4{0.0, 0.0, 0.0, 0.0};  // no tile: always define (keeps acc dead between iterations)
     } else {
+      const int t = wave + NW * s;
       const int I = IJ & 0xffff, J = IJ >> 16;
-      const double* ct = Cc + (size_t)t * 256 + lane;
+      const size_t off = (size_t)t * 256 + lane;
       const int col = 16 * J + (lane & 15);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        double v = ct[64 * r];
+        double v = Cc[off + 64 * r];
+        const double da = DA[off + 64 * r], db = DB[off + 64 * r];
         const int row = 16 * I + (lane >> 4) + 4 * r;
         if (row < a.d && col < a.d) {
           const int j = row / n, aa = row - j * n;
           const int l = col / n, bb = col - l * n;
-          v -= a.alpha * (D[l * a.P + j] * Es[(l * n + aa) * n + bb] + D[j * a.P + l] * Es[(j * n + bb) * n + aa]);
+          v -= da * Es[(l * n + aa) * n + bb] + db * Es[(j * n + bb) * n + aa];
           if (j == l) v += FtE[(j * n + aa) * n + bb];
           if (!MEAS::LINEAR) {
             double s2 = 0.0;
@@ -410,18 +502,18 @@ __device__ __forceinline__ void build_tiles(const GnArgs& a, const ConstLayout& 
         acc[s][r] = v;
       }
     }
+    // bound the scheduler's load hoisting to two slots (register pressure)
+    if (s & 1) __builtin_amdgcn_sched_barrier(0);
   }
 }
 
 // Load H tiles from a dense (dp x dp) matrix (MODE_LINSOLVE).
 template <int SLOTS>
-__device__ __forceinline__ void load_tiles(const GnArgs& a, const int* tab, const double* Hb, d4 (&acc)[SLOTS], int wave, int lane) {
-  // tab: LDS table with -1 sentinels
+__device__ __forceinline__ void load_tiles(const GnArgs& a, const double* Hb, d4 (&acc)[SLOTS], int lane, int stab) {
   const int dp = 16 * a.NT;
 #pragma unroll
   for (int s = 0; s < SLOTS; ++s) {
-    const int t = wave + NW * s;
-    const int IJ = tile_IJ(tab, t);
+    const int IJ = slot_ij(stab, s);
     if (IJ < 0) {
       acc[s] = d4{0.0, 0.0, 0.0, 0.0};
     } else {
@@ -439,44 +531,43 @@ __device__ __forceinline__ void load_tiles(const GnArgs& a, const int* tab, cons
 // fused (BV <- y).  L stays in the tile registers.  Returns false if a pivot
 // was not positive/finite.
 template <int SLOTS>
-__device__ __forceinline__ bool factor_forward(const GnArgs& a, const int* tab, const SmemLayout& SL, double* sm,
-                                               d4 (&acc)[SLOTS], int wave, int lane) {
+__device__ __forceinline__ bool factor_forward(const GnArgs& a, const SmemLayout& SL, double* sm,
+                                               d4 (&acc)[SLOTS], int wave, int lane, int stab, DIAG_FDECL) {
   double* BV = sm + SL.BV;
+  double* YV = sm + SL.YV;
   double* IDG = sm + SL.IDG;
   int* flag = (int*)(sm + SL.RED + 4 * NW);
-  if (threadIdx.x == 0) flag[0] = 0;
   const int NT = a.NT;
-  // lane-dependent LDS offsets shared by every slot
-  const int c_off = ((lane >> 4) * PBS + (lane & 15));   // C-layout element (row g, col c)
-  const int ab_off = ((lane & 15) * PBS + (lane >> 4));  // MFMA A/B operand (row l&15, k l>>4)
+  bool bad = false;
 #pragma unroll 1
   for (int k = 0; k < NT; ++k) {
-    // opaque per-step copies: keep LICM from hoisting 23 slot predicates and
+    // opaque per-step copies: keep LICM from hoisting 23 decoded slots and
     // 16 lane masks out of the step loop (they would spill SGPRs)
-    int lane_o = lane, wave_o = wave;
+    int lane_o = lane, wave_o = wave, stab_o = stab;
     asm volatile("" : "+v"(lane_o));
     asm volatile("" : "+s"(wave_o));
+    asm volatile("" : "+v"(stab_o));
+    const int c_off = ((lane_o >> 4) * PBS + (lane_o & 15));   // C-layout element (row g, col c)
+    const int ab_off = ((lane_o & 15) * PBS + (lane_o >> 4));  // MFMA A/B operand (row l&15, k l>>4)
     double* PB = sm + ((k & 1) ? SL.PB1 : SL.PB0);
     // (1) panel k -> LDS
 #pragma unroll
     for (int s = 0; s < SLOTS; ++s) {
-      const int t = wave_o + NW * s;
-      {
-        const int IJ = tile_IJ(tab, t);
-        const int I = IJ & 0xffff, J = IJ >> 16;
-        if (J == k) {
-          double* dst = PB + (I - k) * 16 * PBS + c_off;
+      const int IJ = slot_ij(stab_o, s);
+      const int I = IJ & 0xffff, J = IJ >> 16;
+      if (IJ >= 0 && J == k) {
+        double* dst = PB + (I - k) * 16 * PBS + c_off;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) dst[4 * r * PBS] = acc[s][r];
-        }
+        for (int r = 0; r < 4; ++r) dst[4 * r * PBS] = acc[s][r];
       }
-      __builtin_amdgcn_sched_barrier(0);
     }
+    DIAG_MARK(8);
     __syncthreads();
+    DIAG_MARK(9);
     // (2) panel sweep: row per lane; every wave redundantly holds the 16
     //     diagonal-block rows in lanes 0..15, lanes 16..63 take 48 panel rows each.
     {
-      const int prow = (lane_o < 16) ? lane : 16 + wave_o * 48 + (lane_o - 16);
+      const int prow = (lane_o < 16) ? lane_o : 16 + wave_o * 48 + (lane_o - 16);
       const bool valid = prow < 16 * (NT - k);
       const bool mine = (lane_o < 16) ? (wave_o == 0) : valid;
       // lanes past the panel read row 0 (finite data) and never write back
@@ -491,17 +582,12 @@ __device__ __forceinline__ bool factor_forward(const GnArgs& a, const int* tab, 
       }
       double bb = BV[16 * k + lrow];
       double myrs = 0.0;
-      bool bad = false;
 #pragma unroll
       for (int c = 0; c < 16; ++c) {
-        double piv = readlane_d(r[c], c);
-        if (!(piv > 0.0) || !isfinite(piv)) {
-          bad = true;
-          piv = 1.0;
-        }
+        const double piv = readlane_d(r[c], c);
+        bad |= !(piv > 0.0 && piv < INFINITY);  // off the critical path: a bad pivot poisons the factor
         const double rs = rsqrt(piv);
-        const double sq = piv * rs;
-        r[c] = (lane_o == c) ? sq : r[c] * rs;
+        r[c] = (lane_o == c) ? piv * rs : r[c] * rs;
         const double yc = readlane_d(bb, c) * rs;
         if (lane_o == c) {
           myrs = rs;
@@ -515,94 +601,99 @@ __device__ __forceinline__ bool factor_forward(const GnArgs& a, const int* tab, 
           r[s2] -= r[c] * Lsc;
         }
       }
+      // Every wave read the diagonal rows (and their RHS) above, so the factored
+      // diagonal block and y_k go to buffers nobody reads in this step (LKK, YV);
+      // panel rows below the diagonal are private to their lane.
       if (mine) {
-        double* dst = PB + prow * PBS;
+        double* dst = (lane_o < 16) ? (sm + SL.LKK + lane_o * PBS) : (PB + prow * PBS);
 #pragma unroll
         for (int c = 0; c < 16; c += 2) *(double2*)(dst + c) = make_double2(r[c], r[c + 1]);
-        BV[16 * k + prow] = bb;
-        if (lane_o < 16) IDG[16 * k + lane] = myrs;
+        if (lane_o < 16) {
+          YV[16 * k + lane_o] = bb;
+          IDG[16 * k + lane_o] = myrs;
+        } else {
+          BV[16 * k + prow] = bb;
+        }
       }
-      if (bad && wave_o == 0 && lane_o == 0) flag[0] = 1;
     }
+    DIAG_MARK(10);
     __syncthreads();
+    DIAG_MARK(11);
     // (3) reload the factored panel into its tiles; trailing update with MFMA
 #pragma unroll
     for (int s = 0; s < SLOTS; ++s) {
-      const int t = wave_o + NW * s;
-      {
-        const int IJ = tile_IJ(tab, t);
-        const int I = IJ & 0xffff, J = IJ >> 16;
-        if (J == k) {
-          const double* srcp = PB + (I - k) * 16 * PBS + c_off;
+      const int IJ = slot_ij(stab_o, s);
+      const int I = IJ & 0xffff, J = IJ >> 16;
+      if (IJ >= 0 && J == k) {
+        const double* srcp = (I == k ? sm + SL.LKK : PB + (I - k) * 16 * PBS) + c_off;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int tr = (lane >> 4) + 4 * r, tc = lane & 15;
-            const double v = srcp[4 * r * PBS];
-            acc[s][r] = (I == k && tr < tc) ? 0.0 : v;
-          }
-        } else if (J > k) {
-          const double* ai = PB + (I - k) * 16 * PBS + ab_off;
-          const double* bj = PB + (J - k) * 16 * PBS + ab_off;
-          double av[4], bv[4];
-#pragma unroll
-          for (int qq = 0; qq < 4; ++qq) {
-            av[qq] = ai[4 * qq];
-            bv[qq] = bj[4 * qq];
-          }
-#pragma unroll
-          for (int qq = 0; qq < 4; ++qq)
-            acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(-av[qq], bv[qq], acc[s], 0, 0, 0);
+        for (int r = 0; r < 4; ++r) {
+          const int tr = (lane_o >> 4) + 4 * r, tc = lane_o & 15;
+          const double v = srcp[4 * r * PBS];
+          acc[s][r] = (I == k && tr < tc) ? 0.0 : v;
         }
+      } else if (IJ >= 0 && J > k) {
+        const double* ai = PB + (I - k) * 16 * PBS + ab_off;
+        const double* bj = PB + (J - k) * 16 * PBS + ab_off;
+        double av[4], bv[4];
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+          av[qq] = ai[4 * qq];
+          bv[qq] = bj[4 * qq];
+        }
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq)
+          acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(-av[qq], bv[qq], acc[s], 0, 0, 0);
       }
-      __builtin_amdgcn_sched_barrier(0);
     }
+    DIAG_MARK(12);
   }
+  if (bad && lane == 0) flag[0] = 1;  // flag was zeroed before the first barrier of this call
   __syncthreads();
   return flag[0] == 0;
 }
 
-// Backward solve L^T delta = y (y in BV) -> DV.
+// Backward solve L^T delta = y (y in BV) -> DV, reading L from the tile registers.
 template <int SLOTS>
-__device__ __forceinline__ void backward(const GnArgs& a, const int* tab, const SmemLayout& SL, double* sm,
-                                         d4 (&acc)[SLOTS], int wave, int lane) {
-  const double* BV = sm + SL.BV;
+__device__ __forceinline__ void backward(const GnArgs& a, const SmemLayout& SL, double* sm,
+                                         d4 (&acc)[SLOTS], int wave, int lane, int stab) {
   const double* IDG = sm + SL.IDG;
-  double* DV = sm + SL.DV;
+  double* DV = sm + SL.YV;  // y on entry; delta_k overwrites y_k (read only by block k)
   double* PART = sm + SL.PART;
   double* LK = sm + SL.PB0;  // 16 x PBS scratch
   const int NT = a.NT;
-  const int c_off = ((lane >> 4) * PBS + (lane & 15));
 #pragma unroll 1
   for (int k = NT - 1; k >= 0; --k) {
-    int lane_o = lane, wave_o = wave;
+    int lane_o = lane, wave_o = wave, stab_o = stab;
     asm volatile("" : "+v"(lane_o));
     asm volatile("" : "+s"(wave_o));
+    asm volatile("" : "+v"(stab_o));
+    const int c_off = ((lane_o >> 4) * PBS + (lane_o & 15));
     double pv = 0.0;
 #pragma unroll
     for (int s = 0; s < SLOTS; ++s) {
-      const int t = wave_o + NW * s;
-      {
-        const int IJ = tile_IJ(tab, t);
-        const int I = IJ & 0xffff, J = IJ >> 16;
-        if (J == k) {
-          if (I > k) {
-            const double* dv = DV + 16 * I + (lane >> 4);
+      const int IJ = slot_ij(stab_o, s);
+      const int I = IJ & 0xffff, J = IJ >> 16;
+      if (IJ >= 0 && J == k) {
+        if (I > k) {
+          const double* dv = DV + 16 * I + (lane_o >> 4);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) pv += acc[s][r] * dv[4 * r];
-          } else {
+          for (int r = 0; r < 4; ++r) pv += acc[s][r] * dv[4 * r];
+        } else {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) LK[c_off + 4 * r * PBS] = acc[s][r];
-          }
+          for (int r = 0; r < 4; ++r) LK[c_off + 4 * r * PBS] = acc[s][r];
         }
       }
-      __builtin_amdgcn_sched_barrier(0);
     }
     pv += __shfl_xor(pv, 16);
     pv += __shfl_xor(pv, 32);
-    if (lane < 16) PART[wave * 16 + lane] = pv;
+    if (lane_o < 16) PART[wave_o * 16 + lane_o] = pv;
     __syncthreads();
     if (wave_o == 0 && lane_o < 16) {
-      double rhs = BV[16 * k + lane_o];
+      double lk[16];
+#pragma unroll
+      for (int s2 = 0; s2 < 16; ++s2) lk[s2] = LK[s2 * PBS + lane_o];  // column lane_o of L_kk
+      double rhs = DV[16 * k + lane_o];
 #pragma unroll
       for (int w = 0; w < NW; ++w) rhs -= PART[w * 16 + lane_o];
       const double idg = IDG[16 * k + lane_o];
@@ -610,7 +701,7 @@ __device__ __forceinline__ void backward(const GnArgs& a, const int* tab, const 
       for (int s2 = 15; s2 >= 0; --s2) {
         const double ds = readlane_d(rhs, s2) * readlane_d(idg, s2);
         if (lane_o == s2) rhs = ds;
-        else if (lane_o < s2) rhs -= LK[s2 * PBS + lane_o] * ds;
+        else if (lane_o < s2) rhs -= lk[s2] * ds;
       }
       DV[16 * k + lane_o] = rhs;
     }
@@ -627,13 +718,10 @@ __global__ __launch_bounds__(NTHREADS, 2) void k_gn(GnArgs a) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int b = blockIdx.x;
-  int* tab = (int*)(sm + SL.TAB);
-  {
-    const int* gtab = (const int*)(a.cbuf + CL.tab);
-    for (int t = threadIdx.x; t < NW * MAX_SLOTS; t += NTHREADS) tab[t] = (t < a.ntiles) ? gtab[t] : -1;
-  }
+  const int stab = make_slot_table(wave, lane, a.NT, a.ntiles);
   double* Xs = sm + SL.Xs;
-  double* DV = sm + SL.DV;
+  if (threadIdx.x == 0) *(int*)(sm + SL.RED + 4 * NW) = 0;  // NOT_SPD flag
+  double* DV = sm + SL.YV;  // delta after backward()
   double* RED = sm + SL.RED;
   d4 acc[SLOTS];
 #pragma unroll
@@ -644,10 +732,11 @@ __global__ __launch_bounds__(NTHREADS, 2) void k_gn(GnArgs a) {
     const int dp = 16 * a.NT;
     const double* Hb = a.Hin + (size_t)b * dp * dp;
     for (int t = threadIdx.x; t < dp; t += NTHREADS) sm[SL.BV + t] = -a.gin[(size_t)b * dp + t];
-    load_tiles<SLOTS>(a, tab, Hb, acc, wave, lane);
+    load_tiles<SLOTS>(a, Hb, acc, lane, stab);
     __syncthreads();
-    const bool ok = factor_forward<SLOTS>(a, tab, SL, sm, acc, wave, lane);
-    backward<SLOTS>(a, tab, SL, sm, acc, wave, lane);
+    DIAG_DECL
+    const bool ok = factor_forward<SLOTS>(a, SL, sm, acc, wave, lane, stab, DIAG_FARGS);
+    backward<SLOTS>(a, SL, sm, acc, wave, lane, stab);
     for (int t = threadIdx.x; t < dp; t += NTHREADS) a.dout[(size_t)b * dp + t] = DV[t];
     if (threadIdx.x == 0) a.status[b] = ok ? MHE_STATUS_CONVERGED : MHE_STATUS_NOT_SPD;
     return;
@@ -658,22 +747,25 @@ __global__ __launch_bounds__(NTHREADS, 2) void k_gn(GnArgs a) {
 
   int status = MHE_STATUS_MAX_ITER;
   int it = 0;
+  DIAG_DECL
   for (;;) {
+    DIAG_MARK(7);
     double c1 = node_phase<DYN>(a, CL, SL, sm, b);
     c1 += meas_phase<DYN, MEAS>(a, CL, SL, sm, b);
     __syncthreads();
+    DIAG_MARK(0);
     c1 += grad_phase<DYN>(a, CL, SL, sm, b);
+    DIAG_MARK(1);
     if constexpr (mode == MODE_ASSEMBLE) {
       double c2 = 0.0;
       block_reduce2(RED, c1, c2, false);
-      build_tiles<DYN, MEAS, SLOTS>(a, CL, SL, sm, acc, wave, lane);
+      build_tiles<DYN, MEAS, SLOTS>(a, CL, SL, sm, acc, wave, lane, stab);
       const int dp = 16 * a.NT;
       double* Hb = a.Hout + (size_t)b * dp * dp;
 #pragma unroll
       for (int s = 0; s < SLOTS; ++s) {
-        const int t = wave + NW * s;
-        if (t < a.ntiles) {
-          const int IJ = tile_IJ(tab, t);
+        const int IJ = slot_ij(stab, s);
+        if (IJ >= 0) {
           const int I = IJ & 0xffff, J = IJ >> 16;
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
@@ -688,17 +780,21 @@ __global__ __launch_bounds__(NTHREADS, 2) void k_gn(GnArgs a) {
       return;
     }
     if (it >= a.max_iter) break;
-    build_tiles<DYN, MEAS, SLOTS>(a, CL, SL, sm, acc, wave, lane);
+    build_tiles<DYN, MEAS, SLOTS>(a, CL, SL, sm, acc, wave, lane, stab);
     __syncthreads();
-    const bool ok = factor_forward<SLOTS>(a, tab, SL, sm, acc, wave, lane);
+    DIAG_MARK(2);
+    const bool ok = factor_forward<SLOTS>(a, SL, sm, acc, wave, lane, stab, DIAG_FARGS);
+    DIAG_MARK(3);
     if (!ok) {
       status = MHE_STATUS_NOT_SPD;
       break;
     }
-    backward<SLOTS>(a, tab, SL, sm, acc, wave, lane);
+    backward<SLOTS>(a, SL, sm, acc, wave, lane, stab);
+    DIAG_MARK(4);
     double dmax = 0.0, xmax = 0.0;
     bool finite = true;
-    for (int t = threadIdx.x; t < a.d; t += NTHREADS) {
+    const int tid_u = opaque_tid();
+    for (int t = tid_u; t < a.d; t += NTHREADS) {
       const double dv = DV[t];
       finite = finite && isfinite(dv);
       dmax = fmax(dmax, fabs(dv));
@@ -709,7 +805,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void k_gn(GnArgs a) {
       status = MHE_STATUS_NONFINITE;
       break;
     }
-    for (int t = threadIdx.x; t < a.d; t += NTHREADS) {
+    for (int t = tid_u; t < a.d; t += NTHREADS) {
       const double xv = Xs[t] + DV[t];
       Xs[t] = xv;
       xmax = fmax(xmax, fabs(xv));
@@ -742,6 +838,8 @@ __global__ __launch_bounds__(NTHREADS, 2) void k_gn(GnArgs a) {
     if (threadIdx.x == 0) a.cost[b] = cf;
   }
 done:
+  DIAG_MARK(5);
+  DIAG_FLUSH(b);
   __syncthreads();
   for (int t = threadIdx.x; t < a.d; t += NTHREADS) a.Xout[(size_t)b * a.d + t] = Xs[t];
   if (threadIdx.x == 0) {
@@ -787,10 +885,14 @@ __global__ void k_build_cc(int P, int M, int n, int p, int NT, int has_prior, do
   }
   double* Cc = (double*)(cbuf + CL.Cc);
   Cc[(size_t)t * 256 + r * 64 + lane] = v;
-  if (e == 0) {
-    int* tab = (int*)(cbuf + CL.tab);
-    tab[t] = I | (J << 16);
+  double da = 0.0, db = 0.0;
+  if (row < d && col < d) {
+    const int j = row / n, l = col / n;
+    da = alpha * D[l * P + j];
+    db = alpha * D[j * P + l];
   }
+  ((double*)(cbuf + CL.DA))[(size_t)t * 256 + r * 64 + lane] = da;
+  ((double*)(cbuf + CL.DB))[(size_t)t * 256 + r * 64 + lane] = db;
 }
 
 __global__ void k_copy_consts(int P, int M, int n, int p, int NT, const double* D, const double* cw,
@@ -825,6 +927,10 @@ __global__ void k_copy_consts(int P, int M, int n, int p, int NT, const double* 
 
 // ================================================================ dispatch
 using namespace mhe;
+
+#ifdef MHE_DIAG
+static unsigned long long* g_dbg = nullptr;
+#endif
 
 namespace {
 
@@ -887,7 +993,8 @@ int smem_bytes(const mhe_dims* dm, int NT) {
 
 template <class DYN, class MEAS>
 int launch_gn(const mhe_dims* dm, GnArgs& a, int batch, int mode, hipStream_t st) {
-  const int smem = smem_bytes(dm, a.NT);
+  int smem = smem_bytes(dm, a.NT);
+  if (const char* pad = getenv("MHE_DEBUG_SMEM_PAD")) smem += atoi(pad);  // debug: force occupancy
   if (smem > 160 * 1024) return MHE_ERR_UNSUPPORTED;
   void (*kern)(GnArgs) = nullptr;
   if (mode == MODE_SOLVE) kern = k_gn<DYN, MEAS, MAX_SLOTS, MODE_SOLVE>;
@@ -944,6 +1051,9 @@ int dispatch(const mhe_dims* dm, F&& f) {
 
 GnArgs make_args(const mhe_dims* dm, const void* cbuf, int NT) {
   GnArgs a = {};
+#ifdef MHE_DIAG
+  a.dbg = g_dbg;
+#endif
   a.cbuf = (const char*)cbuf;
   a.P = dm->N + 1;
   a.M = dm->M;
@@ -977,6 +1087,10 @@ struct LaunchGN {
 };
 
 }  // namespace
+
+#ifdef MHE_DIAG
+extern "C" void mhe_diag_set_buffer(void* p) { g_dbg = (unsigned long long*)p; }
+#endif
 
 extern "C" {
 

@@ -157,3 +157,18 @@ def test_c2_full_batch_properties():
     sub = np.arange(0, 1024, 128)
     Xr, cr, ir, sr = gn.gauss_newton(pb, w.X_init[sub], _U(w)[sub], w.Y[sub], max_iter=30, tol=1e-9)
     assert np.abs(X.cpu().numpy()[sub] - Xr).max() <= 1e-8 * (1 + np.abs(Xr).max())
+
+
+def test_bitwise_deterministic_full_occupancy():
+    """Two workgroups per CU (B=1024) stress intra-workgroup LDS hand-offs: the same
+    inputs must give bitwise-identical results run to run (a race shows up here first)."""
+    w = configs.make_c2(B=1024)
+    s = solver.from_workload(w)
+    r1 = [t.cpu().numpy() for t in s.solve(w.X_init, w.U, w.Y, max_iter=3, tol=0.0)]
+    r2 = [t.cpu().numpy() for t in s.solve(w.X_init, w.U, w.Y, max_iter=3, tol=0.0)]
+    for a, b in zip(r1, r2):
+        assert np.array_equal(a, b)
+    H, g, _ = s.assemble(w.X_init, w.U, w.Y)
+    d1, s1 = s.chol_solve(H, g)
+    d2, s2 = s.chol_solve(H, g)
+    assert torch.equal(d1, d2) and (s1.cpu().numpy() == 0).all()
