@@ -34,7 +34,11 @@ constexpr int NTHREADS = NW * 64;
 constexpr int PBS = 18;            // panel-buffer row stride (doubles): 144 B, 16-B aligned,
                                    // conflict-free for the MFMA operand reads
 constexpr int MAX_NT = 13;         // padded system <= 208 (register-resident path)
-constexpr int MAX_SLOTS = (MAX_NT * (MAX_NT + 1) / 2 + NW - 1) / NW;  // 23
+// The NT(NT-1)/2 off-diagonal tiles live in MFMA accumulator registers (20
+// slots per wave at NT = 13, 160 VGPRs); the NT diagonal tiles live in LDS.
+// Holding all 91 tiles in registers (23 slots) left too few registers for the
+// rest of the kernel and the allocator spilled tiles to scratch.
+constexpr int MAX_SLOTS = (MAX_NT * (MAX_NT - 1) / 2 + NW - 1) / NW;  // 20
 
 enum Mode { MODE_SOLVE = 0, MODE_ASSEMBLE = 1, MODE_LINSOLVE = 2 };
 
@@ -65,7 +69,7 @@ __host__ __device__ inline ConstLayout const_layout(int P, int M, int n, int p, 
 }
 
 struct SmemLayout {  // offsets in doubles
-  int Xs, Vs, FtV, Es, FtE, GE, G, BV, YV, IDG, PB0, PB1, LKK, PART, RED, total;
+  int Xs, Vs, FtV, Es, FtE, GE, G, BV, YV, IDG, PB, DT, LKK, PART, RED, total;
 };
 
 __host__ __device__ inline int rnd2(int x) { return (x + 1) & ~1; }  // keep 16-B alignment
@@ -84,8 +88,8 @@ __host__ __device__ inline SmemLayout smem_layout(int P, int M, int n, int NT, b
   S.BV = o;   o += dp;          // working right-hand side (panel sweeps update it row-wise)
   S.YV = o;   o += dp;          // y = L^-1 (-g), then delta = L^-T y in place
   S.IDG = o;  o += dp;          // 1 / L_cc
-  S.PB0 = o;  o += dp * PBS;    // panel buffers (double-buffered over steps)
-  S.PB1 = o;  o += dp * PBS;
+  S.PB = o;   o += dp * PBS;    // panel buffer: sub-diagonal rows of the current block column
+  S.DT = o;   o += NT * 256;    // diagonal tiles, row-major 16 x 16 (L_kk after step k)
   S.LKK = o;  o += 16 * PBS;    // factored diagonal block of the current step
   S.PART = o; o += NW * 16;
   S.RED = o;  o += 4 * NW + 8;
@@ -176,20 +180,23 @@ __device__ __forceinline__ void block_reduce2(double* red, double& a, double& b,
   b = rb;
 }
 
-// Slot table: lane s of every wave holds (I | J << 16) of the tile in its slot
-// s (tile t = wave + NW*s, column-major over the lower triangle), -1 = none.
-// A slot's coordinates are one v_readlane away (no memory round trip); callers
-// pass an opaque per-step copy so LICM cannot hoist 23 decoded values.
-__device__ __forceinline__ int make_slot_table(int wave, int lane, int NT, int ntiles) {
-  const int t = wave + NW * lane;
-  if (lane >= MAX_SLOTS || t >= ntiles) return -1;
+// Slot table: lane s of every wave holds (I | J << 16) of the off-diagonal
+// tile in its slot s (u = wave + NW*s over the tiles I > J, column-major), or
+// -1.  A slot's coordinates are one v_readlane away (no memory round trip);
+// callers pass an opaque per-step copy so LICM cannot hoist decoded values.
+__device__ __forceinline__ int make_slot_table(int wave, int lane, int NT) {
+  const int u = wave + NW * lane;
+  if (lane >= MAX_SLOTS || u >= NT * (NT - 1) / 2) return -1;
   int J = 0, base = 0;
-  while (t >= base + (NT - J)) {
-    base += NT - J;
+  while (u >= base + (NT - 1 - J)) {
+    base += NT - 1 - J;
     ++J;
   }
-  return (J + (t - base)) | (J << 16);
+  return (J + 1 + (u - base)) | (J << 16);
 }
+
+// linear index of tile (I, J), I >= J, in the column-major lower triangle (Cc/DA/DB layout)
+__device__ __forceinline__ int tile_index(int I, int J, int NT) { return J * NT - J * (J - 1) / 2 + (I - J); }
 
 __device__ __forceinline__ int slot_ij(int stab, int s) { return __builtin_amdgcn_readlane(stab, s); }
 
@@ -453,16 +460,37 @@ __device__ __forceinline__ double grad_phase(const GnArgs& a, const ConstLayout&
   return cost;
 }
 
+// One 16x16 tile element of H at (row, col) in the MFMA C-layout position of
+// this lane (see build_tiles).
+template <class DYN, class MEAS>
+__device__ __forceinline__ double h_element(const GnArgs& a, const double* Phi, const double* Es,
+                                            const double* FtE, const double* G, double v, double da,
+                                            double db, int row, int col) {
+  constexpr int n = DYN::n;
+  if (row < a.d && col < a.d) {
+    const int j = row / n, aa = row - j * n;
+    const int l = col / n, bb = col - l * n;
+    v -= da * Es[(l * n + aa) * n + bb] + db * Es[(j * n + bb) * n + aa];
+    if (j == l) v += FtE[(j * n + aa) * n + bb];
+    if (!MEAS::LINEAR) {
+      double s2 = 0.0;
+      for (int i = 0; i < a.M; ++i) s2 += Phi[i * a.P + j] * Phi[i * a.P + l] * G[(i * n + aa) * n + bb];
+      v += s2;
+    }
+  }
+  return v;
+}
+
 // Build the H tiles owned by this wave:
 //   H = Cc (constant: a^2 (D^T C D) (x) Qw  + linear-measurement term + prior + padding I)
 //     - a D_lj E_l[a,b] - a D_jl E_j[b,a] + delta_jl (F^T E)_j[a,b]      (dynamics, X-dependent)
 //     + sum_i Phi_ij Phi_il G_i[a,b]                                      (nonlinear measurements)
 // Cc, DA = a D_lj and DB = a D_jl are stored per tile element in the MFMA
-// C-layout, so each is one coalesced 512-B load per register.
+// C-layout, so each is one coalesced 512-B load per register.  Off-diagonal
+// tiles go to the accumulator slots, diagonal tiles (owner wave J % NW) to LDS.
 template <class DYN, class MEAS, int SLOTS>
 __device__ __forceinline__ void build_tiles(const GnArgs& a, const ConstLayout& CL, const SmemLayout& SL, double* sm,
                                             d4 (&acc)[SLOTS], int wave, int lane, int stab) {
-  constexpr int n = DYN::n;
   const double* Cc = (const double*)(a.cbuf + CL.Cc);
   const double* DA = (const double*)(a.cbuf + CL.DA);
   const double* DB = (const double*)(a.cbuf + CL.DB);
@@ -479,37 +507,36 @@ __device__ __forceinline__ void build_tiles(const GnArgs& a, const ConstLayout& 
     if (IJ < 0) {
       acc[s] = d4{0.0, 0.0, 0.0, 0.0};  // no tile: always define (keeps acc dead between iterations)
     } else {
-      const int t = wave + NW * s;
       const int I = IJ & 0xffff, J = IJ >> 16;
-      const size_t off = (size_t)t * 256 + lane;
+      const size_t off = (size_t)tile_index(I, J, a.NT) * 256 + lane;
       const int col = 16 * J + (lane & 15);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        double v = Cc[off + 64 * r];
-        const double da = DA[off + 64 * r], db = DB[off + 64 * r];
         const int row = 16 * I + (lane >> 4) + 4 * r;
-        if (row < a.d && col < a.d) {
-          const int j = row / n, aa = row - j * n;
-          const int l = col / n, bb = col - l * n;
-          v -= da * Es[(l * n + aa) * n + bb] + db * Es[(j * n + bb) * n + aa];
-          if (j == l) v += FtE[(j * n + aa) * n + bb];
-          if (!MEAS::LINEAR) {
-            double s2 = 0.0;
-            for (int i = 0; i < a.M; ++i) s2 += Phi[i * a.P + j] * Phi[i * a.P + l] * G[(i * n + aa) * n + bb];
-            v += s2;
-          }
-        }
-        acc[s][r] = v;
+        acc[s][r] = h_element<DYN, MEAS>(a, Phi, Es, FtE, G, Cc[off + 64 * r], DA[off + 64 * r],
+                                         DB[off + 64 * r], row, col);
       }
     }
     // bound the scheduler's load hoisting to two slots (register pressure)
     if (s & 1) __builtin_amdgcn_sched_barrier(0);
   }
+  double* DT = sm + SL.DT;
+  for (int J = wave; J < a.NT; J += NW) {
+    const size_t off = (size_t)tile_index(J, J, a.NT) * 256 + lane;
+    const int col = 16 * J + (lane & 15);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int tr = (lane >> 4) + 4 * r;
+      DT[J * 256 + tr * 16 + (lane & 15)] = h_element<DYN, MEAS>(a, Phi, Es, FtE, G, Cc[off + 64 * r], DA[off + 64 * r],
+                                                                 DB[off + 64 * r], 16 * J + tr, col);
+    }
+  }
 }
 
 // Load H tiles from a dense (dp x dp) matrix (MODE_LINSOLVE).
 template <int SLOTS>
-__device__ __forceinline__ void load_tiles(const GnArgs& a, const double* Hb, d4 (&acc)[SLOTS], int lane, int stab) {
+__device__ __forceinline__ void load_tiles(const GnArgs& a, const SmemLayout& SL, double* sm, const double* Hb,
+                                           d4 (&acc)[SLOTS], int wave, int lane, int stab) {
   const int dp = 16 * a.NT;
 #pragma unroll
   for (int s = 0; s < SLOTS; ++s) {
@@ -525,38 +552,54 @@ __device__ __forceinline__ void load_tiles(const GnArgs& a, const double* Hb, d4
       }
     }
   }
+  double* DT = sm + SL.DT;
+  for (int J = wave; J < a.NT; J += NW)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int tr = (lane >> 4) + 4 * r;
+      DT[J * 256 + tr * 16 + (lane & 15)] = Hb[(size_t)(16 * J + tr) * dp + 16 * J + (lane & 15)];
+    }
 }
 
-// Right-looking blocked Cholesky H = L L^T with the forward solve L y = BV
-// fused (BV <- y).  L stays in the tile registers.  Returns false if a pivot
-// was not positive/finite.
+// Right-looking blocked Cholesky H = L L^T with the forward solve L y = -g
+// fused (YV <- y).  Off-diagonal L tiles stay in the accumulator registers,
+// diagonal L tiles in LDS (DT).  Per block column k:
+//   (1) owners write the sub-diagonal tiles (I, k) to the panel buffer PB;
+//   (2) panel sweep, one row per lane: every wave redundantly factors the
+//       16 diagonal rows (lanes 0..15, read from DT[k]); lanes 16..63 carry
+//       48 sub-diagonal panel rows each; the RHS rides along as a 17th column;
+//   (3) reload L_Ik, trailing update A_IJ -= L_Ik L_Jk^T with
+//       v_mfma_f64_16x16x4f64 (diagonal tiles through LDS).
+// Returns false if a pivot was not positive and finite.
 template <int SLOTS>
 __device__ __forceinline__ bool factor_forward(const GnArgs& a, const SmemLayout& SL, double* sm,
                                                d4 (&acc)[SLOTS], int wave, int lane, int stab, DIAG_FDECL) {
   double* BV = sm + SL.BV;
   double* YV = sm + SL.YV;
   double* IDG = sm + SL.IDG;
+  double* PB = sm + SL.PB;
+  double* DT = sm + SL.DT;
+  double* LKK = sm + SL.LKK;
   int* flag = (int*)(sm + SL.RED + 4 * NW);
   const int NT = a.NT;
   bool bad = false;
 #pragma unroll 1
   for (int k = 0; k < NT; ++k) {
-    // opaque per-step copies: keep LICM from hoisting 23 decoded slots and
-    // 16 lane masks out of the step loop (they would spill SGPRs)
+    // opaque per-step copies: keep LICM from hoisting decoded slots and lane
+    // masks out of the step loop (they would spill)
     int lane_o = lane, wave_o = wave, stab_o = stab;
     asm volatile("" : "+v"(lane_o));
     asm volatile("" : "+s"(wave_o));
     asm volatile("" : "+v"(stab_o));
     const int c_off = ((lane_o >> 4) * PBS + (lane_o & 15));   // C-layout element (row g, col c)
     const int ab_off = ((lane_o & 15) * PBS + (lane_o >> 4));  // MFMA A/B operand (row l&15, k l>>4)
-    double* PB = sm + ((k & 1) ? SL.PB1 : SL.PB0);
-    // (1) panel k -> LDS
+    // (1) sub-diagonal tiles of block column k -> PB rows (I-k-1)*16 ..
 #pragma unroll
     for (int s = 0; s < SLOTS; ++s) {
       const int IJ = slot_ij(stab_o, s);
       const int I = IJ & 0xffff, J = IJ >> 16;
       if (IJ >= 0 && J == k) {
-        double* dst = PB + (I - k) * 16 * PBS + c_off;
+        double* dst = PB + (I - k - 1) * 16 * PBS + c_off;
 #pragma unroll
         for (int r = 0; r < 4; ++r) dst[4 * r * PBS] = acc[s][r];
       }
@@ -564,77 +607,75 @@ __device__ __forceinline__ bool factor_forward(const GnArgs& a, const SmemLayout
     DIAG_MARK(8);
     __syncthreads();
     DIAG_MARK(9);
-    // (2) panel sweep: row per lane; every wave redundantly holds the 16
-    //     diagonal-block rows in lanes 0..15, lanes 16..63 take 48 panel rows each.
+    // (2) panel sweep
     {
-      const int prow = (lane_o < 16) ? lane_o : 16 + wave_o * 48 + (lane_o - 16);
-      const bool valid = prow < 16 * (NT - k);
+      const int sub = wave_o * 48 + (lane_o - 16);          // sub-diagonal panel row of lanes >= 16
+      const bool valid = (lane_o < 16) || (sub < 16 * (NT - 1 - k));
       const bool mine = (lane_o < 16) ? (wave_o == 0) : valid;
-      // lanes past the panel read row 0 (finite data) and never write back
-      const int lrow = valid ? prow : 0;
+      // lanes past the panel read panel row 0 (finite data) and never write back
+      const double* src = (lane_o < 16) ? (DT + k * 256 + lane_o * 16) : (PB + (valid ? sub : 0) * PBS);
       double r[16];
-      const double* src = PB + lrow * PBS;
 #pragma unroll
       for (int c = 0; c < 16; c += 2) {
         const double2 v = *(const double2*)(src + c);
         r[c] = v.x;
         r[c + 1] = v.y;
       }
-      double bb = BV[16 * k + lrow];
-      double myrs = 0.0;
+      double bb = BV[(lane_o < 16) ? 16 * k + lane_o : (valid ? 16 * (k + 1) + sub : 0)];
 #pragma unroll
       for (int c = 0; c < 16; ++c) {
         const double piv = readlane_d(r[c], c);
         bad |= !(piv > 0.0 && piv < INFINITY);  // off the critical path: a bad pivot poisons the factor
         const double rs = rsqrt(piv);
-        r[c] = (lane_o == c) ? piv * rs : r[c] * rs;
+        const double rc = r[c] * rs;
+        r[c] = (lane_o == c) ? piv * rs : rc;
         const double yc = readlane_d(bb, c) * rs;
-        if (lane_o == c) {
-          myrs = rs;
-          bb = yc;
-        } else if (lane_o > c) {
-          bb -= r[c] * yc;
-        }
+        bb = (lane_o == c) ? yc : ((lane_o > c) ? bb - rc * yc : bb);
 #pragma unroll
         for (int s2 = c + 1; s2 < 16; ++s2) {
-          const double Lsc = readlane_d(r[c], s2);
-          r[s2] -= r[c] * Lsc;
+          const double Lsc = readlane_d(rc, s2);
+          r[s2] -= rc * Lsc;
         }
       }
       // Every wave read the diagonal rows (and their RHS) above, so the factored
       // diagonal block and y_k go to buffers nobody reads in this step (LKK, YV);
-      // panel rows below the diagonal are private to their lane.
+      // sub-diagonal panel rows are private to their lane.
       if (mine) {
-        double* dst = (lane_o < 16) ? (sm + SL.LKK + lane_o * PBS) : (PB + prow * PBS);
+        double* dst = (lane_o < 16) ? (LKK + lane_o * PBS) : (PB + sub * PBS);
 #pragma unroll
         for (int c = 0; c < 16; c += 2) *(double2*)(dst + c) = make_double2(r[c], r[c + 1]);
         if (lane_o < 16) {
           YV[16 * k + lane_o] = bb;
-          IDG[16 * k + lane_o] = myrs;
         } else {
-          BV[16 * k + prow] = bb;
+          BV[16 * (k + 1) + sub] = bb;
         }
       }
     }
     DIAG_MARK(10);
     __syncthreads();
     DIAG_MARK(11);
-    // (3) reload the factored panel into its tiles; trailing update with MFMA
+    // (3) L_kk -> DT[k] (upper triangle zeroed, 1/L_cc -> IDG); reload the
+    //     factored panel into its tiles; trailing update with MFMA
+    if (wave_o == k % NW) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int tr = (lane_o >> 4) + 4 * r, tc = lane_o & 15;
+        const double v = LKK[tr * PBS + tc];
+        DT[k * 256 + tr * 16 + tc] = (tr < tc) ? 0.0 : v;
+        if (tr == tc) IDG[16 * k + tc] = 1.0 / v;
+      }
+    }
 #pragma unroll
     for (int s = 0; s < SLOTS; ++s) {
       const int IJ = slot_ij(stab_o, s);
       const int I = IJ & 0xffff, J = IJ >> 16;
       if (IJ >= 0 && J == k) {
-        const double* srcp = (I == k ? sm + SL.LKK : PB + (I - k) * 16 * PBS) + c_off;
+        const double* srcp = PB + (I - k - 1) * 16 * PBS + c_off;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int tr = (lane_o >> 4) + 4 * r, tc = lane_o & 15;
-          const double v = srcp[4 * r * PBS];
-          acc[s][r] = (I == k && tr < tc) ? 0.0 : v;
-        }
+        for (int r = 0; r < 4; ++r) acc[s][r] = srcp[4 * r * PBS];
       } else if (IJ >= 0 && J > k) {
-        const double* ai = PB + (I - k) * 16 * PBS + ab_off;
-        const double* bj = PB + (J - k) * 16 * PBS + ab_off;
+        const double* ai = PB + (I - k - 1) * 16 * PBS + ab_off;
+        const double* bj = PB + (J - k - 1) * 16 * PBS + ab_off;
         double av[4], bv[4];
 #pragma unroll
         for (int qq = 0; qq < 4; ++qq) {
@@ -646,21 +687,38 @@ __device__ __forceinline__ bool factor_forward(const GnArgs& a, const SmemLayout
           acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(-av[qq], bv[qq], acc[s], 0, 0, 0);
       }
     }
+    // diagonal tiles J > k owned by this wave: A_JJ -= L_Jk L_Jk^T through LDS
+    for (int J = wave_o; J < NT; J += NW) {
+      if (J <= k) continue;
+      d4 t;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) t[r] = DT[J * 256 + ((lane_o >> 4) + 4 * r) * 16 + (lane_o & 15)];
+      const double* aj = PB + (J - k - 1) * 16 * PBS + ab_off;
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        const double v = aj[4 * qq];
+        t = __builtin_amdgcn_mfma_f64_16x16x4f64(-v, v, t, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) DT[J * 256 + ((lane_o >> 4) + 4 * r) * 16 + (lane_o & 15)] = t[r];
+    }
     DIAG_MARK(12);
+    __syncthreads();  // PB is single-buffered: the next step's panel write waits for these reads
   }
-  if (bad && lane == 0) flag[0] = 1;  // flag was zeroed before the first barrier of this call
+  if (bad && lane == 0) flag[0] = 1;  // flag was zeroed at kernel start
   __syncthreads();
   return flag[0] == 0;
 }
 
-// Backward solve L^T delta = y (y in BV) -> DV, reading L from the tile registers.
+// Backward solve L^T delta = y (YV) -> delta in place, reading the
+// off-diagonal L tiles from the accumulator registers and L_kk from LDS.
 template <int SLOTS>
 __device__ __forceinline__ void backward(const GnArgs& a, const SmemLayout& SL, double* sm,
                                          d4 (&acc)[SLOTS], int wave, int lane, int stab) {
   const double* IDG = sm + SL.IDG;
+  const double* DT = sm + SL.DT;
   double* DV = sm + SL.YV;  // y on entry; delta_k overwrites y_k (read only by block k)
   double* PART = sm + SL.PART;
-  double* LK = sm + SL.PB0;  // 16 x PBS scratch
   const int NT = a.NT;
 #pragma unroll 1
   for (int k = NT - 1; k >= 0; --k) {
@@ -668,21 +726,15 @@ __device__ __forceinline__ void backward(const GnArgs& a, const SmemLayout& SL, 
     asm volatile("" : "+v"(lane_o));
     asm volatile("" : "+s"(wave_o));
     asm volatile("" : "+v"(stab_o));
-    const int c_off = ((lane_o >> 4) * PBS + (lane_o & 15));
     double pv = 0.0;
 #pragma unroll
     for (int s = 0; s < SLOTS; ++s) {
       const int IJ = slot_ij(stab_o, s);
       const int I = IJ & 0xffff, J = IJ >> 16;
       if (IJ >= 0 && J == k) {
-        if (I > k) {
-          const double* dv = DV + 16 * I + (lane_o >> 4);
+        const double* dv = DV + 16 * I + (lane_o >> 4);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) pv += acc[s][r] * dv[4 * r];
-        } else {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) LK[c_off + 4 * r * PBS] = acc[s][r];
-        }
+        for (int r = 0; r < 4; ++r) pv += acc[s][r] * dv[4 * r];
       }
     }
     pv += __shfl_xor(pv, 16);
@@ -692,7 +744,7 @@ __device__ __forceinline__ void backward(const GnArgs& a, const SmemLayout& SL, 
     if (wave_o == 0 && lane_o < 16) {
       double lk[16];
 #pragma unroll
-      for (int s2 = 0; s2 < 16; ++s2) lk[s2] = LK[s2 * PBS + lane_o];  // column lane_o of L_kk
+      for (int s2 = 0; s2 < 16; ++s2) lk[s2] = DT[k * 256 + s2 * 16 + lane_o];  // column lane_o of L_kk
       double rhs = DV[16 * k + lane_o];
 #pragma unroll
       for (int w = 0; w < NW; ++w) rhs -= PART[w * 16 + lane_o];
@@ -718,7 +770,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void k_gn(GnArgs a) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int b = blockIdx.x;
-  const int stab = make_slot_table(wave, lane, a.NT, a.ntiles);
+  const int stab = make_slot_table(wave, lane, a.NT);
   double* Xs = sm + SL.Xs;
   if (threadIdx.x == 0) *(int*)(sm + SL.RED + 4 * NW) = 0;  // NOT_SPD flag
   double* DV = sm + SL.YV;  // delta after backward()
@@ -732,7 +784,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void k_gn(GnArgs a) {
     const int dp = 16 * a.NT;
     const double* Hb = a.Hin + (size_t)b * dp * dp;
     for (int t = threadIdx.x; t < dp; t += NTHREADS) sm[SL.BV + t] = -a.gin[(size_t)b * dp + t];
-    load_tiles<SLOTS>(a, Hb, acc, lane, stab);
+    load_tiles<SLOTS>(a, SL, sm, Hb, acc, wave, lane, stab);
     __syncthreads();
     DIAG_DECL
     const bool ok = factor_forward<SLOTS>(a, SL, sm, acc, wave, lane, stab, DIAG_FARGS);
@@ -774,6 +826,11 @@ __global__ __launch_bounds__(NTHREADS, 2) void k_gn(GnArgs a) {
             if (I != J) Hb[(size_t)col * dp + row] = acc[s][r];
           }
         }
+      }
+      __syncthreads();  // diagonal tiles (LDS) complete
+      for (int t = threadIdx.x; t < a.NT * 256; t += NTHREADS) {
+        const int J = t >> 8, tr = (t >> 4) & 15, tc = t & 15;
+        Hb[(size_t)(16 * J + tr) * dp + 16 * J + tc] = sm[SL.DT + t];
       }
       for (int t = threadIdx.x; t < dp; t += NTHREADS) a.gout[(size_t)b * dp + t] = -sm[SL.BV + t];
       if (threadIdx.x == 0) a.cost[b] = c1;
