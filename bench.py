@@ -93,25 +93,20 @@ def main():
     args = ap.parse_args()
 
     import torch
-    import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from mhe import configs, dist, solver
+
+    world, rank, local = dist.world()
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    dist.init("nccl", dev)
 
-    from mhe import configs, solver
-
-    w = configs.make_c2(B=args.batch, seed=1 + 1000 * rank)
+    w = configs.make_c2(B=args.batch, seed=dist.shard_seed(1, rank))
     s = solver.from_workload(w, device=dev)
-    if world > 1:
-        # model constants: built on rank 0, broadcast over RCCL/xGMI (one-time, untimed)
-        dist.broadcast(s.cbuf, src=0)
+    # model constants: rank 0's device buffer broadcast over RCCL/xGMI (one-time, untimed)
+    dist.broadcast_(s.cbuf, src=0)
     staged = s.prepare(w.X_init, w.U, w.Y)
     B = args.batch
     outs = (torch.empty_like(staged[0]), torch.empty(B, dtype=torch.float64, device=dev),
@@ -121,8 +116,7 @@ def main():
     for _ in range(args.warmup):
         s.solve_staged(staged, outs, args.iters, 0.0, stream)
     torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
+    dist.barrier()
     torch.cuda.synchronize(dev)
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
@@ -132,20 +126,13 @@ def main():
         s.solve_staged(staged, outs, args.iters, 0.0, stream)
     ev1.record(stream)
     torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
+    dist.barrier()
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
     kern_ms = ev0.elapsed_time(ev1) / args.steps  # launches are back to back on `stream`
 
-    iters_done = outs[2].sum().item()
-    if world > 1:
-        t = torch.tensor([wall], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        wall = t.item()
-        it = torch.tensor([iters_done], dtype=torch.float64, device=dev)
-        dist.all_reduce(it, op=dist.ReduceOp.SUM)
-        iters_done = it.item()
+    wall = dist.max_over_ranks(wall, dev)
+    iters_done = dist.sum_over_ranks(outs[2].sum().item(), dev)
     total_updates = iters_done * w.P * args.steps  # sum over ranks of B * P * iters per step
     value = total_updates / wall
 
@@ -179,7 +166,8 @@ def main():
             rec["cpu_baseline"] = cpu_baseline(w, args.iters, args.cpu_sample)
         print(json.dumps(rec))
     if world > 1:
-        dist.destroy_process_group()
+        import torch.distributed as tdist
+        tdist.destroy_process_group()
 
 
 if __name__ == "__main__":

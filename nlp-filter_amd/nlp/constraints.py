@@ -1,0 +1,7 @@
+"""Constraint plug-ins -- kingdwd/nlp-filter nlp/constraints.py (signature kept;
+equality constraints are not on the Gauss-Newton hot path)."""
+
+
+def equality_constaint(x, params=None):
+    """x[0] - x[1] (nlp/constraints.py:4-5; the reference's spelling is kept)"""
+    return x[0] - x[1]

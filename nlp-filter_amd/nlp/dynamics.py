@@ -1,0 +1,57 @@
+"""Dynamics plug-ins, reference signatures ``f(x, u, params=None)`` (m > 0) and
+``f(x, params=None)`` (m = 0) -- kingdwd/nlp-filter nlp/dynamics.py.
+
+Host NumPy definitions; the GPU solver maps each registered name to a device
+functor with an analytic Jacobian (csrc/mhe_models.h, mhe.registry)."""
+import numpy as np
+
+from ._ops import cos, sin, tan, vertcat
+
+
+def single_integrator(x, u, params=None):
+    """x = [x], u = [v_x]; xdot = u  (nlp/dynamics.py:4-8)"""
+    return vertcat(u[0])
+
+
+def single_integrator_2D(x, u, params=None):
+    """(nlp/dynamics.py:10-17)"""
+    return vertcat(u[0], u[1])
+
+
+def single_integrator_3D(x, u, params=None):
+    """(nlp/dynamics.py:19-27)"""
+    return vertcat(u[0], u[1], u[2])
+
+
+def double_integrator(x, u, params=None):
+    """x = [x, y, xdot, ydot], u = [a_x, a_y]  (nlp/dynamics.py:29-38)"""
+    return vertcat(x[2], x[3], u[0], u[1])
+
+
+def van_der_pol(x, u, params=None):
+    """x = [x0, x1]  (nlp/dynamics.py:61-66)"""
+    return vertcat((1 - x[1] ** 2) * x[0] - x[1] + u[0], x[0])
+
+
+def gnss_pos_and_bias(x, u, params=None):
+    """x = [x, y, z, b, bd]; xdot = u, bdot = bd  (nlp/dynamics.py:68-79)"""
+    return vertcat(u[0], u[1], u[2], x[4], 0.0)
+
+
+def multi_receiver(x, params=None):
+    """x = [xB, yB, zB, bB, xdB, ydB, zdB, alphaB], m = 0  (nlp/dynamics.py:81-96)"""
+    return vertcat(x[4], x[5], x[6], x[7], 0.0, 0.0, 0.0, 0.0)
+
+
+def gnss_two_receiver(x, u, params=None):
+    """x = [xA, yA, zA, bA, alphaA, xB, yB, zB, bB, alphaB]  (nlp/dynamics.py:98-115)"""
+    return vertcat(u[0], u[1], u[2], x[4], 0.0, u[3], u[4], u[5], x[9], 0.0)
+
+
+def kinematic_bycicle_and_bias(x, u, params=None):
+    """Kinematic bicycle + clock bias (nlp/dynamics.py:117-136).  As in the
+    reference code, x[2] is the angle inside cos/sin."""
+    L = 0.28
+    v = 8.72649116358 * u[0] - 0.856053299155
+    delta = np.deg2rad(28) * u[1]
+    return vertcat(v * cos(x[2]), v * sin(x[2]), 0.0, x[4], 0.0, (v / L) * tan(delta))

@@ -1,0 +1,363 @@
+"""Estimation-NLP builder and solve facade -- drop-in for kingdwd/nlp-filter nlp/nlp.py.
+
+The reference records a CasADi ``Opti`` problem and hands it to IPOPT
+(nlp/nlp.py:61-83).  Here the same calls record a *problem spec*; ``build()``
+turns it into device constants (libmhe.so, ``mhe_build_constants``) and
+``solve()`` runs the batched Gauss-Newton kernel (``mhe_gn_solve``) on the
+GPU.  The process-noise variables ``W`` of ``addDynamics`` are eliminated
+through the collocation equality W_k = (2/T) sum_j D_kj X_j - f(X_k, U_k)
+(nlp/nlp.py:235) -- the unconstrained least-squares problem has the same
+stationary point IPOPT converges to -- and stay extractable by name.
+
+Kept semantics
+  * ``addVariables`` / ``addParameter`` return lists of handles; parameters
+    (controls, measurements, sat positions, weights) can be set later with
+    ``setParameter`` / ``setControl`` / ``setMeasurement`` (nlp/nlp.py:38-56,304-312)
+  * ``R`` passed to ``addResidualCost`` is the *information* matrix
+    (the reference adds r^T R r, nlp/nlp.py:273)
+  * ``solve(warmstart=True)`` starts from the previous solution (nlp/nlp.py:77-79);
+    ``self.solver`` holds IPOPT-style stats incl. ``t_wall_total`` (nlp/nlp.py:83)
+  * ``extractVariableValue`` / ``extractSolution`` print and return None on a
+    missing name or before ``solve()`` (nlp/nlp.py:85-119)
+
+Not on the Gauss-Newton path yet (raise ``UnsupportedFeature``): inequality /
+equality constraints, the pseudo-Huber cost (f2), mixed
+measurement models in one problem, and ``fixedTimeOptimalControlNLP`` (out of
+scope: the north star is the estimator).  ``addVarBounds`` is recorded and
+checked after the solve (``self.solver["bounds_violated"]``) but not enforced.
+"""
+import time
+import warnings
+
+import numpy as np
+from scipy.interpolate import interp1d
+
+from . import collocation
+
+
+class UnsupportedFeature(NotImplementedError):
+    pass
+
+
+class Var:
+    """Decision-variable handle (stands in for ``opti.variable(n)``)."""
+    __slots__ = ("name", "idx", "size", "value", "init")
+
+    def __init__(self, name, idx, size):
+        self.name, self.idx, self.size = name, idx, size
+        self.value = None
+        self.init = None
+
+    def __repr__(self):
+        return f"Var({self.name}_{self.idx}, n={self.size})"
+
+
+class Param:
+    """Parameter handle (stands in for ``opti.parameter(n)``)."""
+    __slots__ = ("size", "value")
+
+    def __init__(self, size, value=None):
+        self.size = size
+        self.value = None if value is None else np.asarray(value, dtype=np.float64).reshape(-1)
+
+    def get(self):
+        if self.value is None:
+            raise ValueError("parameter used before setParameter()")
+        return self.value
+
+
+def _resolve(v):
+    return v.get() if isinstance(v, Param) else v
+
+
+def _fname(f):
+    return getattr(f, "__name__", str(f))
+
+
+class NLP(object):
+    """Variable / parameter bookkeeping and the solve facade (nlp/nlp.py:8-119)."""
+
+    def __init__(self, N):
+        self.N = N
+        self.var_names = []
+        self.var_sizes = []
+        self.w = {}
+        self.sol = None
+        self.solver = None
+        self._bounds = []
+
+    def addVariables(self, N_var, n_var, lb=None, ub=None, name='x'):
+        X = []
+        for i in range(N_var):
+            var_name = name + '_' + str(i)
+            self.var_names.append(var_name)
+            self.var_sizes.append(n_var)
+            x = Var(name, i, n_var)
+            self.w[var_name] = x
+            X.append(x)
+        if lb is not None or ub is not None:
+            self._bounds.append((X, None, lb, ub))
+        return X
+
+    def addParameter(self, N_var, n_var, val=None):
+        return [Param(n_var, val) for _ in range(N_var)]
+
+    def addIneqConstraint(self, g, arguments, params=None):
+        raise UnsupportedFeature("inequality constraints are not on the Gauss-Newton path (SURVEY.md §8 f4)")
+
+    def addEqConstraint(self, h, arguments, params=None):
+        raise UnsupportedFeature("equality constraints are not on the Gauss-Newton path (SURVEY.md §8 f4)")
+
+    def setParameter(self, p, val):
+        if not isinstance(p, Param):
+            raise TypeError("setParameter expects a handle returned by addParameter")
+        p.value = np.asarray(val, dtype=np.float64).reshape(-1)
+
+    def setObjective(self):
+        pass  # the objective is recorded term by term by the add*Cost calls
+
+    def initialGuess(self, x, x0):
+        x.init = np.asarray(x0, dtype=np.float64).reshape(-1)
+
+    def extractVariableValue(self, name, idx=0):
+        var_name = name + '_' + str(idx)
+        if var_name in self.w.keys():
+            if self.sol is not None:
+                return np.array(self.w[var_name].value, dtype=np.float64).reshape(-1)
+            print('Need to run solve() first')
+            return None
+        print('Could not find ' + name + '_' + str(idx) + '.')
+        return None
+
+    def extractSolution(self, name, t_array):
+        X = []
+        for i in range(self.N + 1):
+            value = self.extractVariableValue(name, i)
+            if value is None:
+                return None
+            X.append(value)
+        T = len(t_array)
+        sol = np.zeros((T, X[0].shape[0]))
+        for t in range(T):
+            sol[t, :] = self.CPM.evaluateSolution(t_array[t], X)
+        return sol
+
+
+class fixedTimeOptimalControlNLP(NLP):
+    def __init__(self, N, T, n, m):
+        raise UnsupportedFeature(
+            "fixedTimeOptimalControlNLP (nlp/nlp.py:122-186) is out of scope: this framework "
+            "accelerates the estimation path (fixedTimeOptimalEstimationNLP)")
+
+
+class fixedTimeOptimalEstimationNLP(NLP):
+    """Moving-horizon / collocation estimation problem (nlp/nlp.py:189-317)."""
+
+    def __init__(self, N, T, n, m, phi_mode="bary", device="cuda"):
+        super(fixedTimeOptimalEstimationNLP, self).__init__(N)
+        self.T = T
+        self.n = n
+        self.m = m
+        self.CPM = collocation.ChebyshevPseudospectralMethod(self.N, 0, T, phi_mode=phi_mode)
+        self.device = device
+        self._dyn = None
+        self._dyn_cost = None
+        self._meas = []
+        self._prior = None
+        self._X = None
+        self._engine = None
+        self._engine_key = None
+        self.max_iter = 50
+        self.tol = 1e-10
+
+    # ------------------------------------------------------------ recording
+    def addVariables(self, N_var, n_var, lb=None, ub=None, name='x'):
+        X = super().addVariables(N_var, n_var, lb, ub, name)
+        if name == 'x' and self._X is None:
+            self._X = X
+        return X
+
+    def addDynamics(self, func, X, t_array=None, u_array=None, params=None):
+        """nlp/nlp.py:202-240 -> (U, W); W is eliminated (see module docstring)."""
+        if len(X) != self.N + 1:
+            print('X must have N+1 points defined.')
+        self._X = X
+        U = self.addParameter(self.N + 1, self.m) if self.m != 0 else None
+        if self.m == 0:
+            print('No control input being used for dynamics.')
+        W = super().addVariables(self.N + 1, self.n, name='w')
+        self._dyn = (func, params, U, W)
+        if u_array is not None:
+            self.setControl(U, t_array, u_array)
+        return U, W
+
+    def addDynamicsCost(self, cost_function, W, params=None):
+        """nlp/nlp.py:242-245: sum_k (T/2) w_k c(W_k)."""
+        name = _fname(cost_function)
+        if name == "weighted_l2_norm":
+            Qw = np.asarray(_resolve(params["Q"]), dtype=np.float64).reshape(self.n, self.n)
+        elif name == "l2_norm":
+            Qw = np.eye(self.n)
+        else:
+            raise UnsupportedFeature(f"dynamics cost {name!r}: the Gauss-Newton path needs a least-squares "
+                                     "cost (weighted_l2_norm / l2_norm); pseudo_huber_loss is SURVEY.md §8 f2")
+        self._dyn_cost = Qw
+
+    def addResidualCost(self, measurement_model, X, t_array, y_array, R, params=None):
+        """nlp/nlp.py:247-277: sum_i r_i^T R r_i, r_i = y_i - h(x(t_i), params)."""
+        t_array = np.asarray(t_array, dtype=np.float64).reshape(-1)
+        M_i = t_array.shape[0]
+        p = y_array.shape[0] if y_array is not None else int(params["p"])
+        Y = self.addParameter(M_i, p)
+        self._meas.append(dict(h=measurement_model, t=t_array, Y=Y, R=R, params=params or {}, p=p))
+        if y_array is not None:
+            self.setMeasurement(Y, t_array, y_array)
+        return Y
+
+    def addInitialCost(self, cost_function, X0, params=None, x0=None):
+        """nlp/nlp.py:279-286: c(X_0 - x0_guess)."""
+        name = _fname(cost_function)
+        if name == "weighted_l2_norm":
+            Pw = params["Q"]
+        elif name == "l2_norm":
+            Pw = np.eye(self.n)
+        else:
+            raise UnsupportedFeature(f"initial cost {name!r} is not least-squares")
+        x0_guess = self.addParameter(1, self.n)[0]
+        self._prior = (Pw, x0_guess)
+        if x0 is not None:
+            self.setParameter(x0_guess, x0)
+        return x0_guess
+
+    def initializeEstimate(self, X, t_array, xhat_array):
+        """nlp/nlp.py:288-302: interp1d of xhat (n, T) at the node times."""
+        t_nodes = self.CPM.tau2t(self.CPM.tau)
+        xhat_nodes = interp1d(t_array, xhat_array, fill_value="extrapolate")(t_nodes)
+        for (i, x) in enumerate(X):
+            self.initialGuess(x, xhat_nodes[:, i])
+
+    def setControl(self, U, t_array, u_array):
+        """nlp/nlp.py:304-308: linear interp1d with extrapolation at tau2t(tau_k)."""
+        u_t = interp1d(t_array, u_array, fill_value="extrapolate")
+        for k in range(self.N + 1):
+            self.setParameter(U[k], u_t(self.CPM.tau2t(self.CPM.tau[k])))
+
+    def setMeasurement(self, Y, t_array, y_array):
+        """nlp/nlp.py:310-312"""
+        for (i, t) in enumerate(t_array):
+            self.setParameter(Y[i], np.asarray(y_array)[:, i])
+
+    def addVarBounds(self, X, idx, lb, ub):
+        """Recorded and checked after solve(); not enforced."""
+        self._bounds.append((X, idx, lb, ub))
+
+    # ------------------------------------------------------------ assembly
+    def _spec(self):
+        if self._dyn is None:
+            raise ValueError("addDynamics() must be called before build()")
+        if self._dyn_cost is None:
+            raise ValueError("addDynamicsCost() must be called before build()")
+        if not self._meas:
+            raise ValueError("at least one addResidualCost() term is required")
+        names = {_fname(g["h"]) for g in self._meas}
+        if len(names) != 1:
+            raise UnsupportedFeature(f"one measurement model per problem on the GPU path, got {sorted(names)}")
+        mname = names.pop()
+        t_meas, Rw, PAR, idx = [], [], [], None
+        for g in self._meas:
+            R = np.asarray(_resolve(g["R"]), dtype=np.float64).reshape(g["p"], g["p"])
+            par = g["params"]
+            row_par = None
+            if mname in ("pseudorange", "vehicle_pseudorange"):
+                row_par = np.asarray(_resolve(par["sat_pos"]), dtype=np.float64).reshape(3)
+                if "idx" in par:
+                    idx = list(par["idx"])
+            elif mname == "multi_receiver_range_3d":
+                if "y" not in par:
+                    raise UnsupportedFeature("multi_receiver_range_3d between two state blocks (idxA/idxB)")
+                row_par = np.asarray(_resolve(par["y"]), dtype=np.float64).reshape(3)
+                idx = list(par.get("idx", [0, 1, 2]))
+            for t in g["t"]:
+                t_meas.append(t)
+                Rw.append(R)
+                if row_par is not None:
+                    PAR.append(row_par)
+        return mname, np.asarray(t_meas), np.stack(Rw), (np.stack(PAR) if PAR else None), idx
+
+    def build(self, verbose=True):
+        """Build the device constants (nlp/nlp.py:61-69)."""
+        from mhe import solver as _solver
+        mname, t_meas, Rw, PAR, idx = self._spec()
+        func = self._dyn[0]
+        Phi = self.CPM.lagrange_matrix(t_meas)
+        Pw = None if self._prior is None else np.asarray(_resolve(self._prior[0]), dtype=np.float64)
+        key = (Rw.tobytes(), None if Pw is None else Pw.tobytes(), self._dyn_cost.tobytes())
+        if self._engine is None or self._engine_key != key:
+            self._engine = _solver.BatchSolver(self.N, self.T, func, mname, self.CPM.D, (self.T / 2.0) * self.CPM.w,
+                                               Phi, self._dyn_cost, Rw, Pw=Pw, meas_idx=idx, device=self.device)
+            self._engine_key = key
+        self._PAR = PAR
+
+    def batch_solver(self):
+        """The BatchSolver of this problem structure (many trajectories at once)."""
+        if self._engine is None:
+            self.build()
+        return self._engine
+
+    # ------------------------------------------------------------ solve
+    def solve(self, warmstart=False):
+        """Gauss-Newton on the GPU (replaces opti.solve(), nlp/nlp.py:76-83)."""
+        if warmstart and self.sol is not None:
+            print('Warmstarting with previous solution')
+        self.build()  # cheap when nothing changed; picks up re-set R / prior weights
+        eng = self._engine
+        P, n = self.N + 1, self.n
+        X0 = np.zeros((1, P, n))
+        for k, x in enumerate(self._X):
+            if warmstart and self.sol is not None and x.value is not None:
+                X0[0, k] = x.value
+            elif x.init is not None:
+                X0[0, k] = x.init
+        U = None
+        if self.m > 0:
+            U = np.stack([u.get() for u in self._dyn[2]])[None]
+        Y = np.concatenate([np.stack([y.get() for y in g["Y"]]) for g in self._meas])[None]
+        PAR = None if self._PAR is None else self._PAR[None]
+        x0 = None if self._prior is None else self._prior[1].get()[None]
+        import torch
+        t0 = time.perf_counter()
+        X, cost, iters, status = eng.solve(X0, U, Y, PAR, x0, max_iter=self.max_iter, tol=self.tol)
+        torch.cuda.synchronize()
+        t_wall = time.perf_counter() - t0
+        X = X.cpu().numpy()[0]
+        st = int(status.cpu().numpy()[0])
+        for k, x in enumerate(self._X):
+            x.value = X[k].copy()
+        # W eliminated: W_k = (2/T) sum_j D_kj X_j - f(X_k, U_k)  (nlp/nlp.py:235)
+        func, dparams, Uh, W = self._dyn
+        for k, wv in enumerate(W):
+            f = func(X[k], Uh[k].get(), dparams) if self.m > 0 else func(X[k], dparams)
+            wv.value = (2.0 / self.T) * (self.CPM.D[k] @ X) - np.asarray(f, dtype=np.float64).reshape(-1)
+        self.sol = {v: self.w[v].value for v in self.var_names}
+        statuses = {0: "Solve_Succeeded", 1: "Maximum_Iterations_Exceeded", 2: "Not_Positive_Definite",
+                    3: "Invalid_Number_Detected"}
+        self.solver = {"t_wall_total": t_wall, "iter_count": int(iters.cpu().numpy()[0]),
+                       "return_status": statuses[st], "success": st == 0,
+                       "objective": float(cost.cpu().numpy()[0]), "bounds_violated": self._check_bounds()}
+        if st != 0:
+            warnings.warn(f"Gauss-Newton solve ended with {statuses[st]}")
+
+    def _check_bounds(self):
+        viol = False
+        for X, idx, lb, ub in self._bounds:
+            for x in X:
+                if x.value is None:
+                    continue
+                v = x.value if idx is None else x.value[idx]
+                if lb is not None and np.any(v < np.asarray(lb) - 1e-9):
+                    viol = True
+                if ub is not None and np.any(v > np.asarray(ub) + 1e-9):
+                    viol = True
+        if viol:
+            warnings.warn("solution violates a recorded variable bound (bounds are not enforced yet)")
+        return viol
