@@ -31,8 +31,6 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 
 constexpr int NW = 4;              // waves per workgroup (one trajectory)
 constexpr int NTHREADS = NW * 64;
-constexpr int PBS = 18;            // panel-buffer row stride (doubles): 144 B, 16-B aligned,
-                                   // conflict-free for the MFMA operand reads
 constexpr int MAX_NT = 13;         // padded system <= 208 (register-resident path)
 // The NT(NT-1)/2 off-diagonal tiles live in MFMA accumulator registers (20
 // slots per wave at NT = 13, 160 VGPRs); the NT diagonal tiles live in LDS.
@@ -69,10 +67,13 @@ __host__ __device__ inline ConstLayout const_layout(int P, int M, int n, int p, 
 }
 
 struct SmemLayout {  // offsets in doubles
-  int Xs, Vs, FtV, Es, FtE, GE, G, BV, YV, IDG, PB, DT, LKK, PART, RED, total;
+  int Xs, Vs, FtV, Es, FtE, GE, G, BV, YV, PB, DT, RED, total;
 };
 
 __host__ __device__ inline int rnd2(int x) { return (x + 1) & ~1; }  // keep 16-B alignment
+
+constexpr int DTS = 272;  // diagonal-tile stride: A_kk row-major (256), then L_kk^-T with row stride 17
+constexpr int LIS = 17;   // row stride of L_kk^-T (conflict-free row and column reads)
 
 __host__ __device__ inline SmemLayout smem_layout(int P, int M, int n, int NT, bool nonlinear) {
   SmemLayout S;
@@ -85,13 +86,10 @@ __host__ __device__ inline SmemLayout smem_layout(int P, int M, int n, int NT, b
   S.FtE = o;  o += rnd2(P * n * n);
   S.GE = o;   o += rnd2(M * n);
   S.G = o;    o += nonlinear ? rnd2(M * n * n) : 0;
-  S.BV = o;   o += dp;          // working right-hand side (panel sweeps update it row-wise)
-  S.YV = o;   o += dp;          // y = L^-1 (-g), then delta = L^-T y in place
-  S.IDG = o;  o += dp;          // 1 / L_cc
-  S.PB = o;   o += dp * PBS;    // panel buffer: sub-diagonal rows of the current block column
-  S.DT = o;   o += NT * 256;    // diagonal tiles, row-major 16 x 16 (L_kk after step k)
-  S.LKK = o;  o += 16 * PBS;    // factored diagonal block of the current step
-  S.PART = o; o += NW * 16;
+  S.BV = o;   o += dp;                  // right-hand side b = -g, updated block by block
+  S.YV = o;   o += dp;                  // y = U^-T b, then delta = U^-1 y in place
+  S.PB = o;   o += (NT - 1) * 256;      // block row k of U (tiles U_kb, b > k), register order
+  S.DT = o;   o += NT * DTS;            // diagonal blocks
   S.RED = o;  o += 4 * NW + 8;
   S.total = o;
   return S;
@@ -481,7 +479,10 @@ __device__ __forceinline__ double h_element(const GnArgs& a, const double* Phi, 
   return v;
 }
 
-// Build the H tiles owned by this wave:
+// Build the H tiles owned by this wave.  Slot (I, J), I > J, holds the UPPER
+// block H[J-block][I-block] in the MFMA C layout (lane l, register r: row
+// (l>>4)+4r, column l&15); in that layout the tile is directly the B operand
+// (and the transposed A operand) of v_mfma_f64_16x16x4f64 -- see factor_forward.
 //   H = Cc (constant: a^2 (D^T C D) (x) Qw  + linear-measurement term + prior + padding I)
 //     - a D_lj E_l[a,b] - a D_jl E_j[b,a] + delta_jl (F^T E)_j[a,b]      (dynamics, X-dependent)
 //     + sum_i Phi_ij Phi_il G_i[a,b]                                      (nonlinear measurements)
@@ -509,10 +510,10 @@ __device__ __forceinline__ void build_tiles(const GnArgs& a, const ConstLayout& 
     } else {
       const int I = IJ & 0xffff, J = IJ >> 16;
       const size_t off = (size_t)tile_index(I, J, a.NT) * 256 + lane;
-      const int col = 16 * J + (lane & 15);
+      const int col = 16 * I + (lane & 15);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = 16 * I + (lane >> 4) + 4 * r;
+        const int row = 16 * J + (lane >> 4) + 4 * r;
         acc[s][r] = h_element<DYN, MEAS>(a, Phi, Es, FtE, G, Cc[off + 64 * r], DA[off + 64 * r],
                                          DB[off + 64 * r], row, col);
       }
@@ -527,7 +528,7 @@ __device__ __forceinline__ void build_tiles(const GnArgs& a, const ConstLayout& 
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int tr = (lane >> 4) + 4 * r;
-      DT[J * 256 + tr * 16 + (lane & 15)] = h_element<DYN, MEAS>(a, Phi, Es, FtE, G, Cc[off + 64 * r], DA[off + 64 * r],
+      DT[J * DTS + tr * 16 + (lane & 15)] = h_element<DYN, MEAS>(a, Phi, Es, FtE, G, Cc[off + 64 * r], DA[off + 64 * r],
                                                                  DB[off + 64 * r], 16 * J + tr, col);
     }
   }
@@ -547,7 +548,7 @@ __device__ __forceinline__ void load_tiles(const GnArgs& a, const SmemLayout& SL
       const int I = IJ & 0xffff, J = IJ >> 16;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = 16 * I + (lane >> 4) + 4 * r, col = 16 * J + (lane & 15);
+        const int row = 16 * J + (lane >> 4) + 4 * r, col = 16 * I + (lane & 15);
         acc[s][r] = Hb[(size_t)row * dp + col];
       }
     }
@@ -557,205 +558,274 @@ __device__ __forceinline__ void load_tiles(const GnArgs& a, const SmemLayout& SL
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int tr = (lane >> 4) + 4 * r;
-      DT[J * 256 + tr * 16 + (lane & 15)] = Hb[(size_t)(16 * J + tr) * dp + 16 * J + (lane & 15)];
+      DT[J * DTS + tr * 16 + (lane & 15)] = Hb[(size_t)(16 * J + tr) * dp + 16 * J + (lane & 15)];
     }
 }
 
-// Right-looking blocked Cholesky H = L L^T with the forward solve L y = -g
-// fused (YV <- y).  Off-diagonal L tiles stay in the accumulator registers,
-// diagonal L tiles in LDS (DT).  Per block column k:
-//   (1) owners write the sub-diagonal tiles (I, k) to the panel buffer PB;
-//   (2) panel sweep, one row per lane: every wave redundantly factors the
-//       16 diagonal rows (lanes 0..15, read from DT[k]); lanes 16..63 carry
-//       48 sub-diagonal panel rows each; the RHS rides along as a 17th column;
-//   (3) reload L_Ik, trailing update A_IJ -= L_Ik L_Jk^T with
-//       v_mfma_f64_16x16x4f64 (diagonal tiles through LDS).
-// Returns false if a pivot was not positive and finite.
+// LDS ordering between lanes of ONE wave: LDS operations of a wave execute in
+// order, so a compiler-level fence plus a wait on the wave's own stores suffices.
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Sum of v over the 16 lanes of a DPP row (lanes with equal l >> 4), result in
+// every lane of the row: xor 1, xor 2 (quad_perm), half-mirror, mirror.
+__device__ __forceinline__ double row16_sum(double v) {
+#define MHE_DPP_ADD(ctrl)                                                                   \
+  {                                                                                         \
+    const long long bits = __double_as_longlong(v);                                         \
+    const int lo = __builtin_amdgcn_mov_dpp((int)bits, ctrl, 0xF, 0xF, false);              \
+    const int hi = __builtin_amdgcn_mov_dpp((int)(bits >> 32), ctrl, 0xF, 0xF, false);      \
+    v += __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);                    \
+  }
+  MHE_DPP_ADD(0xB1)   // quad_perm [1,0,3,2]
+  MHE_DPP_ADD(0x4E)   // quad_perm [2,3,0,1]
+  MHE_DPP_ADD(0x141)  // row_half_mirror
+  MHE_DPP_ADD(0x140)  // row_mirror
+#undef MHE_DPP_ADD
+  return v;
+}
+
+// Panel of block k, run by ONE wave (look-ahead: during the previous step's
+// trailing update).  On entry DT[k] holds the fully updated A_kk (row-major)
+// and bk the fully updated b_k.  One right-looking elimination in which the
+// same register index j carries three things, one per lane role:
+//   lanes  0..15  row i of A_kk:              v[j] = A'_ij
+//   lanes 16..31  column t of the identity:   v[j] = E'_jt
+//   lane  32      the right-hand side:        v[j] = b'_j
+// Pivot c:  rs = 1 / sqrt(A'_cc);  q = v[c] rs  (= L_ic on row lanes, = (L^-1)_ct
+// and y_c on the others, which are final at that point);  then for j > c
+//   v[j] -= q L_jc   with L_jc = q of row lane j (v_readlane),
+// i.e. ONE fma updates the Cholesky trailing row, the forward substitution
+// L Y = I and L y = b together (~580 VALU instructions, ~40 VGPRs).
+// Stores L_kk^-T into DT[k] (row stride LIS) and y_k into yk.
+// Returns true if a pivot was not positive and finite (wave-uniform).
+__device__ __forceinline__ bool panel(double* DTk, const double* bk, double* yk, int lane) {
+  const int i = lane & 15;
+  const bool erow = (lane >= 16 && lane < 32);
+  double v[16];
+#pragma unroll
+  for (int c = 0; c < 16; c += 2) {
+    const double2 a2 = *(const double2*)(DTk + i * 16 + c);
+    const double2 b2 = *(const double2*)(bk + c);
+    v[c] = (lane == 32) ? b2.x : (erow ? (c == i ? 1.0 : 0.0) : a2.x);
+    v[c + 1] = (lane == 32) ? b2.y : (erow ? (c + 1 == i ? 1.0 : 0.0) : a2.y);
+  }
+  bool bad = false;
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    const double piv = readlane_d(v[c], c);
+    bad |= !(piv > 0.0 && piv < INFINITY);
+    const double q = v[c] * rsqrt(piv);
+    v[c] = q;
+#pragma unroll
+    for (int j = c + 1; j < 16; ++j) v[j] -= q * readlane_d(q, j);
+  }
+  if (erow) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) DTk[i * LIS + j] = v[j];  // (L^-T)[t][j] = (L^-1)[j][t]
+  } else if (lane == 32) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) yk[j] = v[j];
+  }
+  return bad;
+}
+
+// Right-looking blocked Cholesky H = U^T U (U = L^T) with the forward solve
+// U^T y = b (b = -g in BV) fused.  Slot (I, J), I > J, holds the upper block
+// H[J][I] in C layout; after step J it holds U_JI.  Per block row k:
+//   T(k)  owners of the tiles (k, b), b > k:  U_kb = L_kk^-1 A_kb  (4 MFMAs, the
+//         tile is the B operand straight from its registers, L_kk^-1 the A
+//         operand from LDS); U_kb -> PB in register order (= row-major).
+//   U(k)  trailing update A_ab -= U_ka^T U_kb (a <= b) with both operands read
+//         row-major from PB, and b_b -= U_kb^T y_k from PB (VALU); the panel
+//         wave (k+1) % NW first finishes b_{k+1} and the diagonal block k+1,
+//         then runs panel(k+1) while the other waves do the remaining tiles
+//         (look-ahead: no separate panel phase).
+// Two workgroup barriers per block row.  Returns false on a bad pivot.
 template <int SLOTS>
 __device__ __forceinline__ bool factor_forward(const GnArgs& a, const SmemLayout& SL, double* sm,
                                                d4 (&acc)[SLOTS], int wave, int lane, int stab, DIAG_FDECL) {
   double* BV = sm + SL.BV;
   double* YV = sm + SL.YV;
-  double* IDG = sm + SL.IDG;
   double* PB = sm + SL.PB;
   double* DT = sm + SL.DT;
-  double* LKK = sm + SL.LKK;
   int* flag = (int*)(sm + SL.RED + 4 * NW);
   const int NT = a.NT;
   bool bad = false;
+  // k = -1 is the prologue: panel(0) only
 #pragma unroll 1
-  for (int k = 0; k < NT; ++k) {
+  for (int k = -1; k + 1 < NT; ++k) {
     // opaque per-step copies: keep LICM from hoisting decoded slots and lane
     // masks out of the step loop (they would spill)
     int lane_o = lane, wave_o = wave, stab_o = stab;
     asm volatile("" : "+v"(lane_o));
     asm volatile("" : "+s"(wave_o));
     asm volatile("" : "+v"(stab_o));
-    const int c_off = ((lane_o >> 4) * PBS + (lane_o & 15));   // C-layout element (row g, col c)
-    const int ab_off = ((lane_o & 15) * PBS + (lane_o >> 4));  // MFMA A/B operand (row l&15, k l>>4)
-    // (1) sub-diagonal tiles of block column k -> PB rows (I-k-1)*16 ..
+    // ---- T(k): U_kb = L_kk^-1 A_kb for the tiles (k, b) of this wave -> registers and PB
+    if (k >= 0) {
+      const double* LT = DT + k * DTS;
+      double la[4];
 #pragma unroll
-    for (int s = 0; s < SLOTS; ++s) {
-      const int IJ = slot_ij(stab_o, s);
-      const int I = IJ & 0xffff, J = IJ >> 16;
-      if (IJ >= 0 && J == k) {
-        double* dst = PB + (I - k - 1) * 16 * PBS + c_off;
+      for (int r = 0; r < 4; ++r) la[r] = LT[(4 * r + (lane_o >> 4)) * LIS + (lane_o & 15)];  // L^-1[l&15][4r+(l>>4)]
 #pragma unroll
-        for (int r = 0; r < 4; ++r) dst[4 * r * PBS] = acc[s][r];
+      for (int s = 0; s < SLOTS; ++s) {
+        const int IJ = slot_ij(stab_o, s);
+        const int I = IJ & 0xffff, J = IJ >> 16;
+        if (IJ >= 0 && J == k) {
+          d4 u = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+          for (int r = 0; r < 4; ++r) u = __builtin_amdgcn_mfma_f64_16x16x4f64(la[r], acc[s][r], u, 0, 0, 0);
+          acc[s] = u;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) PB[(I - k - 1) * 256 + r * 64 + lane_o] = u[r];
+        }
       }
     }
     DIAG_MARK(8);
     __syncthreads();
     DIAG_MARK(9);
-    // (2) panel sweep
-    {
-      const int sub = wave_o * 48 + (lane_o - 16);          // sub-diagonal panel row of lanes >= 16
-      const bool valid = (lane_o < 16) || (sub < 16 * (NT - 1 - k));
-      const bool mine = (lane_o < 16) ? (wave_o == 0) : valid;
-      // lanes past the panel read panel row 0 (finite data) and never write back
-      const double* src = (lane_o < 16) ? (DT + k * 256 + lane_o * 16) : (PB + (valid ? sub : 0) * PBS);
-      double r[16];
-#pragma unroll
-      for (int c = 0; c < 16; c += 2) {
-        const double2 v = *(const double2*)(src + c);
-        r[c] = v.x;
-        r[c + 1] = v.y;
-      }
-      double bb = BV[(lane_o < 16) ? 16 * k + lane_o : (valid ? 16 * (k + 1) + sub : 0)];
-#pragma unroll
-      for (int c = 0; c < 16; ++c) {
-        const double piv = readlane_d(r[c], c);
-        bad |= !(piv > 0.0 && piv < INFINITY);  // off the critical path: a bad pivot poisons the factor
-        const double rs = rsqrt(piv);
-        const double rc = r[c] * rs;
-        r[c] = (lane_o == c) ? piv * rs : rc;
-        const double yc = readlane_d(bb, c) * rs;
-        bb = (lane_o == c) ? yc : ((lane_o > c) ? bb - rc * yc : bb);
-#pragma unroll
-        for (int s2 = c + 1; s2 < 16; ++s2) {
-          const double Lsc = readlane_d(rc, s2);
-          r[s2] -= rc * Lsc;
-        }
-      }
-      // Every wave read the diagonal rows (and their RHS) above, so the factored
-      // diagonal block and y_k go to buffers nobody reads in this step (LKK, YV);
-      // sub-diagonal panel rows are private to their lane.
-      if (mine) {
-        double* dst = (lane_o < 16) ? (LKK + lane_o * PBS) : (PB + sub * PBS);
-#pragma unroll
-        for (int c = 0; c < 16; c += 2) *(double2*)(dst + c) = make_double2(r[c], r[c + 1]);
+    // ---- U(k)
+    const int pw = (k + 1) % NW;  // panel wave of this step
+    if (wave_o == pw) {
+      double* DTn = DT + (k + 1) * DTS;
+      if (k >= 0) {
+        // b_{k+1} -= U_{k,k+1}^T y_k (needed by the panel)
         if (lane_o < 16) {
-          YV[16 * k + lane_o] = bb;
-        } else {
-          BV[16 * (k + 1) + sub] = bb;
-        }
-      }
-    }
-    DIAG_MARK(10);
-    __syncthreads();
-    DIAG_MARK(11);
-    // (3) L_kk -> DT[k] (upper triangle zeroed, 1/L_cc -> IDG); reload the
-    //     factored panel into its tiles; trailing update with MFMA
-    if (wave_o == k % NW) {
+          double s0 = 0.0, s1 = 0.0;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int tr = (lane_o >> 4) + 4 * r, tc = lane_o & 15;
-        const double v = LKK[tr * PBS + tc];
-        DT[k * 256 + tr * 16 + tc] = (tr < tc) ? 0.0 : v;
-        if (tr == tc) IDG[16 * k + tc] = 1.0 / v;
+          for (int q = 0; q < 16; q += 2) {
+            s0 += PB[q * 16 + lane_o] * YV[16 * k + q];
+            s1 += PB[(q + 1) * 16 + lane_o] * YV[16 * k + q + 1];
+          }
+          BV[16 * (k + 1) + lane_o] -= s0 + s1;
+        }
+        d4 t;
+        double v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          t[r] = DTn[r * 64 + lane_o];
+          v[r] = PB[r * 64 + lane_o];
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) t = __builtin_amdgcn_mfma_f64_16x16x4f64(-v[r], v[r], t, 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) DTn[r * 64 + lane_o] = t[r];
+        wave_lds_sync();
+      }
+      wave_lds_sync();
+      bad |= panel(DTn, BV + 16 * (k + 1), YV + 16 * (k + 1), lane_o);
+    } else if (k >= 0) {
+      // b_b -= U_kb^T y_k for b >= k + 2: one output per lane of the other waves
+      const int vt = ((wave_o - pw - 1 + NW) % NW) * 64 + lane_o;
+      const int bq = k + 2 + (vt >> 4), c = vt & 15;
+      if (bq < NT) {
+        const double* ub = PB + (bq - k - 1) * 256 + c;
+        double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+        for (int q = 0; q < 16; q += 2) {
+          s0 += ub[q * 16] * YV[16 * k + q];
+          s1 += ub[(q + 1) * 16] * YV[16 * k + q + 1];
+        }
+        BV[16 * bq + c] -= s0 + s1;
       }
     }
 #pragma unroll
     for (int s = 0; s < SLOTS; ++s) {
       const int IJ = slot_ij(stab_o, s);
       const int I = IJ & 0xffff, J = IJ >> 16;
-      if (IJ >= 0 && J == k) {
-        const double* srcp = PB + (I - k - 1) * 16 * PBS + c_off;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc[s][r] = srcp[4 * r * PBS];
-      } else if (IJ >= 0 && J > k) {
-        const double* ai = PB + (I - k - 1) * 16 * PBS + ab_off;
-        const double* bj = PB + (J - k - 1) * 16 * PBS + ab_off;
+      if (IJ >= 0 && J > k && k >= 0) {
+        const double* ua = PB + (J - k - 1) * 256 + lane_o;
+        const double* ub = PB + (I - k - 1) * 256 + lane_o;
         double av[4], bv[4];
 #pragma unroll
-        for (int qq = 0; qq < 4; ++qq) {
-          av[qq] = ai[4 * qq];
-          bv[qq] = bj[4 * qq];
+        for (int r = 0; r < 4; ++r) {
+          av[r] = ua[64 * r];
+          bv[r] = ub[64 * r];
         }
 #pragma unroll
-        for (int qq = 0; qq < 4; ++qq)
-          acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(-av[qq], bv[qq], acc[s], 0, 0, 0);
+        for (int r = 0; r < 4; ++r) acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(-av[r], bv[r], acc[s], 0, 0, 0);
       }
     }
-    // diagonal tiles J > k owned by this wave: A_JJ -= L_Jk L_Jk^T through LDS
+    // remaining diagonal blocks J > k + 1 of this wave
     for (int J = wave_o; J < NT; J += NW) {
-      if (J <= k) continue;
+      if (J <= k + 1 || k < 0) continue;
+      double* DTj = DT + J * DTS;
       d4 t;
+      double v[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) t[r] = DT[J * 256 + ((lane_o >> 4) + 4 * r) * 16 + (lane_o & 15)];
-      const double* aj = PB + (J - k - 1) * 16 * PBS + ab_off;
-#pragma unroll
-      for (int qq = 0; qq < 4; ++qq) {
-        const double v = aj[4 * qq];
-        t = __builtin_amdgcn_mfma_f64_16x16x4f64(-v, v, t, 0, 0, 0);
+      for (int r = 0; r < 4; ++r) {
+        t[r] = DTj[r * 64 + lane_o];
+        v[r] = PB[(J - k - 1) * 256 + r * 64 + lane_o];
       }
 #pragma unroll
-      for (int r = 0; r < 4; ++r) DT[J * 256 + ((lane_o >> 4) + 4 * r) * 16 + (lane_o & 15)] = t[r];
+      for (int r = 0; r < 4; ++r) t = __builtin_amdgcn_mfma_f64_16x16x4f64(-v[r], v[r], t, 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) DTj[r * 64 + lane_o] = t[r];
     }
-    DIAG_MARK(12);
-    __syncthreads();  // PB is single-buffered: the next step's panel write waits for these reads
+    DIAG_MARK(10);
+    __syncthreads();  // PB is single-buffered; DT[k+1] / y_{k+1} complete
+    DIAG_MARK(11);
   }
   if (bad && lane == 0) flag[0] = 1;  // flag was zeroed at kernel start
   __syncthreads();
   return flag[0] == 0;
 }
 
-// Backward solve L^T delta = y (YV) -> delta in place, reading the
-// off-diagonal L tiles from the accumulator registers and L_kk from LDS.
+// delta_k = L_kk^-T y_k for lanes 0..15 (row lane of L^-T, y broadcast), in place.
+__device__ __forceinline__ void block_back(const double* LT, double* yv, int lane) {
+  if (lane < 16) {
+    double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+    for (int q = 0; q < 16; q += 2) {
+      s0 += LT[lane * LIS + q] * yv[q];
+      s1 += LT[lane * LIS + q + 1] * yv[q + 1];
+    }
+    const double dv = s0 + s1;
+    wave_lds_sync();  // every lane has read y before any lane overwrites it
+    yv[lane] = dv;
+  }
+}
+
+// Backward solve U delta = y (YV, in place), right-looking over block columns:
+// once delta_b is known, the owners of the tiles (J, b), J < b, subtract
+// U_Jb delta_b from y_J (row sums over the 16 lanes of a DPP row); the owner of
+// (b-1, b) then finishes y_{b-1} and forms delta_{b-1} = L^-T y_{b-1} itself.
+// One workgroup barrier per block.
 template <int SLOTS>
 __device__ __forceinline__ void backward(const GnArgs& a, const SmemLayout& SL, double* sm,
                                          d4 (&acc)[SLOTS], int wave, int lane, int stab) {
-  const double* IDG = sm + SL.IDG;
   const double* DT = sm + SL.DT;
-  double* DV = sm + SL.YV;  // y on entry; delta_k overwrites y_k (read only by block k)
-  double* PART = sm + SL.PART;
+  double* DV = sm + SL.YV;
   const int NT = a.NT;
+  if (wave == (NT - 1) % NW) block_back(DT + (NT - 1) * DTS, DV + 16 * (NT - 1), lane);
+  __syncthreads();
 #pragma unroll 1
-  for (int k = NT - 1; k >= 0; --k) {
-    int lane_o = lane, wave_o = wave, stab_o = stab;
+  for (int bb = NT - 1; bb >= 1; --bb) {
+    int lane_o = lane, stab_o = stab;
     asm volatile("" : "+v"(lane_o));
-    asm volatile("" : "+s"(wave_o));
     asm volatile("" : "+v"(stab_o));
-    double pv = 0.0;
+    const double db = DV[16 * bb + (lane_o & 15)];
 #pragma unroll
     for (int s = 0; s < SLOTS; ++s) {
       const int IJ = slot_ij(stab_o, s);
       const int I = IJ & 0xffff, J = IJ >> 16;
-      if (IJ >= 0 && J == k) {
-        const double* dv = DV + 16 * I + (lane_o >> 4);
+      if (IJ >= 0 && I == bb) {
+        double* yj = DV + 16 * J;
+        double part[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) pv += acc[s][r] * dv[4 * r];
+        for (int r = 0; r < 4; ++r) part[r] = row16_sum(acc[s][r] * db);
+        // lane l of row group g = l>>4 holds the sums for rows g + 4r; lane (l & 15) == r writes row g + 4r
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if ((lane_o & 15) == r) yj[(lane_o >> 4) + 4 * r] -= part[r];
+        if (J == bb - 1) {
+          wave_lds_sync();
+          block_back(DT + J * DTS, yj, lane_o);
+        }
       }
-    }
-    pv += __shfl_xor(pv, 16);
-    pv += __shfl_xor(pv, 32);
-    if (lane_o < 16) PART[wave_o * 16 + lane_o] = pv;
-    __syncthreads();
-    if (wave_o == 0 && lane_o < 16) {
-      double lk[16];
-#pragma unroll
-      for (int s2 = 0; s2 < 16; ++s2) lk[s2] = DT[k * 256 + s2 * 16 + lane_o];  // column lane_o of L_kk
-      double rhs = DV[16 * k + lane_o];
-#pragma unroll
-      for (int w = 0; w < NW; ++w) rhs -= PART[w * 16 + lane_o];
-      const double idg = IDG[16 * k + lane_o];
-#pragma unroll
-      for (int s2 = 15; s2 >= 0; --s2) {
-        const double ds = readlane_d(rhs, s2) * readlane_d(idg, s2);
-        if (lane_o == s2) rhs = ds;
-        else if (lane_o < s2) rhs -= lk[s2] * ds;
-      }
-      DV[16 * k + lane_o] = rhs;
     }
     __syncthreads();
   }
@@ -821,7 +891,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void k_gn(GnArgs a) {
           const int I = IJ & 0xffff, J = IJ >> 16;
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int row = 16 * I + (lane >> 4) + 4 * r, col = 16 * J + (lane & 15);
+            const int row = 16 * J + (lane >> 4) + 4 * r, col = 16 * I + (lane & 15);
             Hb[(size_t)row * dp + col] = acc[s][r];
             if (I != J) Hb[(size_t)col * dp + row] = acc[s][r];
           }
@@ -830,7 +900,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void k_gn(GnArgs a) {
       __syncthreads();  // diagonal tiles (LDS) complete
       for (int t = threadIdx.x; t < a.NT * 256; t += NTHREADS) {
         const int J = t >> 8, tr = (t >> 4) & 15, tc = t & 15;
-        Hb[(size_t)(16 * J + tr) * dp + 16 * J + tc] = sm[SL.DT + t];
+        Hb[(size_t)(16 * J + tr) * dp + 16 * J + tc] = sm[SL.DT + J * DTS + (t & 255)];
       }
       for (int t = threadIdx.x; t < dp; t += NTHREADS) a.gout[(size_t)b * dp + t] = -sm[SL.BV + t];
       if (threadIdx.x == 0) a.cost[b] = c1;
@@ -923,7 +993,8 @@ __global__ void k_build_cc(int P, int M, int n, int p, int NT, int has_prior, do
     ++J;
   }
   const int I = J + (t - base);
-  const int row = 16 * I + (lane >> 4) + 4 * r, col = 16 * J + (lane & 15);
+  // tile t = (I, J), I >= J, stores the upper block H[J-block][I-block] in C layout
+  const int row = 16 * J + (lane >> 4) + 4 * r, col = 16 * I + (lane & 15);
   const int d = P * n;
   double v;
   if (row < d && col < d) {
