@@ -137,6 +137,13 @@ struct GnArgs {
 #define DIAG_FARGS 0
 #endif
 
+// Knock-out build (tools/ko_probe.py): -DMHE_KO=<mask> disables parts of the
+// factorization to measure their cost; results are wrong.  Never in the product.
+#ifndef MHE_KO
+#define MHE_KO 0
+#endif
+#define KO(bit) ((MHE_KO >> (bit)) & 1)
+
 // ------------------------------------------------------------ wave helpers
 __device__ __forceinline__ double readlane_d(double v, int lane) {
   const long long b = __double_as_longlong(v);
@@ -197,6 +204,13 @@ __device__ __forceinline__ int make_slot_table(int wave, int lane, int NT) {
 __device__ __forceinline__ int tile_index(int I, int J, int NT) { return J * NT - J * (J - 1) / 2 + (I - J); }
 
 __device__ __forceinline__ int slot_ij(int stab, int s) { return __builtin_amdgcn_readlane(stab, s); }
+
+// Number of this wave's slots whose tile column is < j (slots are column-major,
+// so the tiles of columns >= j are the slot suffix starting here).
+__device__ __forceinline__ int slot_start(int j, int wave, int NT) {
+  const int base = j * (NT - 1) - j * (j - 1) / 2;  // tiles in columns < j
+  return base > wave ? (base - wave + NW - 1) / NW : 0;
+}
 
 // ------------------------------------------------------------ model phases
 // Mat-vec phases use TPR = 2 threads per row: each sums half of the row with
@@ -479,8 +493,9 @@ __device__ __forceinline__ double h_element(const GnArgs& a, const double* Phi, 
   return v;
 }
 
-// Build the H tiles owned by this wave.  Slot (I, J), I > J, holds the UPPER
-// block H[J-block][I-block] in the MFMA C layout (lane l, register r: row
+// Build the H tiles owned by this wave, NEGATED (the factorization accumulates
+// +U^T U into -A, so no operand needs a sign flip).  Slot (I, J), I > J, holds
+// the UPPER block H[J-block][I-block] in the MFMA C layout (lane l, register r: row
 // (l>>4)+4r, column l&15); in that layout the tile is directly the B operand
 // (and the transposed A operand) of v_mfma_f64_16x16x4f64 -- see factor_forward.
 //   H = Cc (constant: a^2 (D^T C D) (x) Qw  + linear-measurement term + prior + padding I)
@@ -514,8 +529,8 @@ __device__ __forceinline__ void build_tiles(const GnArgs& a, const ConstLayout& 
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = 16 * J + (lane >> 4) + 4 * r;
-        acc[s][r] = h_element<DYN, MEAS>(a, Phi, Es, FtE, G, Cc[off + 64 * r], DA[off + 64 * r],
-                                         DB[off + 64 * r], row, col);
+        acc[s][r] = -h_element<DYN, MEAS>(a, Phi, Es, FtE, G, Cc[off + 64 * r], DA[off + 64 * r],
+                                          DB[off + 64 * r], row, col);
       }
     }
     // bound the scheduler's load hoisting to two slots (register pressure)
@@ -528,8 +543,8 @@ __device__ __forceinline__ void build_tiles(const GnArgs& a, const ConstLayout& 
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int tr = (lane >> 4) + 4 * r;
-      DT[J * DTS + tr * 16 + (lane & 15)] = h_element<DYN, MEAS>(a, Phi, Es, FtE, G, Cc[off + 64 * r], DA[off + 64 * r],
-                                                                 DB[off + 64 * r], 16 * J + tr, col);
+      DT[J * DTS + tr * 16 + (lane & 15)] = -h_element<DYN, MEAS>(a, Phi, Es, FtE, G, Cc[off + 64 * r], DA[off + 64 * r],
+                                                                  DB[off + 64 * r], 16 * J + tr, col);
     }
   }
 }
@@ -549,7 +564,7 @@ __device__ __forceinline__ void load_tiles(const GnArgs& a, const SmemLayout& SL
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = 16 * J + (lane >> 4) + 4 * r, col = 16 * I + (lane & 15);
-        acc[s][r] = Hb[(size_t)row * dp + col];
+        acc[s][r] = -Hb[(size_t)row * dp + col];
       }
     }
   }
@@ -558,7 +573,7 @@ __device__ __forceinline__ void load_tiles(const GnArgs& a, const SmemLayout& SL
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int tr = (lane >> 4) + 4 * r;
-      DT[J * DTS + tr * 16 + (lane & 15)] = Hb[(size_t)(16 * J + tr) * dp + 16 * J + (lane & 15)];
+      DT[J * DTS + tr * 16 + (lane & 15)] = -Hb[(size_t)(16 * J + tr) * dp + 16 * J + (lane & 15)];
     }
 }
 
@@ -590,7 +605,8 @@ __device__ __forceinline__ double row16_sum(double v) {
 
 // Panel of block k, run by ONE wave (look-ahead: during the previous step's
 // trailing update).  On entry DT[k] holds the fully updated A_kk (row-major)
-// and bk the fully updated b_k.  One right-looking elimination in which the
+// (negated, as all tiles) and bk the fully updated b_k.  One right-looking
+// elimination in which the
 // same register index j carries three things, one per lane role:
 //   lanes  0..15  row i of A_kk:              v[j] = A'_ij
 //   lanes 16..31  column t of the identity:   v[j] = E'_jt
@@ -610,8 +626,8 @@ __device__ __forceinline__ bool panel(double* DTk, const double* bk, double* yk,
   for (int c = 0; c < 16; c += 2) {
     const double2 a2 = *(const double2*)(DTk + i * 16 + c);
     const double2 b2 = *(const double2*)(bk + c);
-    v[c] = (lane == 32) ? b2.x : (erow ? (c == i ? 1.0 : 0.0) : a2.x);
-    v[c + 1] = (lane == 32) ? b2.y : (erow ? (c + 1 == i ? 1.0 : 0.0) : a2.y);
+    v[c] = (lane == 32) ? b2.x : (erow ? (c == i ? 1.0 : 0.0) : -a2.x);  // DT holds -A_kk
+    v[c + 1] = (lane == 32) ? b2.y : (erow ? (c + 1 == i ? 1.0 : 0.0) : -a2.y);
   }
   bool bad = false;
 #pragma unroll
@@ -664,21 +680,22 @@ __device__ __forceinline__ bool factor_forward(const GnArgs& a, const SmemLayout
     asm volatile("" : "+v"(lane_o));
     asm volatile("" : "+s"(wave_o));
     asm volatile("" : "+v"(stab_o));
-    // ---- T(k): U_kb = L_kk^-1 A_kb for the tiles (k, b) of this wave -> registers and PB
+    // ---- T(k): U_kb = L_kk^-1 A_kb for the tiles (k, b) of this wave, slots [sT, sU)
+    const int sT = slot_start(k < 0 ? 0 : k, wave_o, NT), sU = slot_start(k + 1, wave_o, NT);
+    const int nS = slot_start(NT - 1, wave_o, NT);
     if (k >= 0) {
       const double* LT = DT + k * DTS;
       double la[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) la[r] = LT[(4 * r + (lane_o >> 4)) * LIS + (lane_o & 15)];  // L^-1[l&15][4r+(l>>4)]
+      for (int r = 0; r < 4; ++r) la[r] = -LT[(4 * r + (lane_o >> 4)) * LIS + (lane_o & 15)];  // -L^-1[l&15][4r+(l>>4)]
 #pragma unroll
       for (int s = 0; s < SLOTS; ++s) {
-        const int IJ = slot_ij(stab_o, s);
-        const int I = IJ & 0xffff, J = IJ >> 16;
-        if (IJ >= 0 && J == k) {
+        if (s >= sT && s < sU) {
           d4 u = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
           for (int r = 0; r < 4; ++r) u = __builtin_amdgcn_mfma_f64_16x16x4f64(la[r], acc[s][r], u, 0, 0, 0);
-          acc[s] = u;
+          if (!KO(0)) acc[s] = u;
+          const int I = slot_ij(stab_o, s) & 0xffff;
 #pragma unroll
           for (int r = 0; r < 4; ++r) PB[(I - k - 1) * 256 + r * 64 + lane_o] = u[r];
         }
@@ -710,14 +727,14 @@ __device__ __forceinline__ bool factor_forward(const GnArgs& a, const SmemLayout
           v[r] = PB[r * 64 + lane_o];
         }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) t = __builtin_amdgcn_mfma_f64_16x16x4f64(-v[r], v[r], t, 0, 0, 0);
+        for (int r = 0; r < 4; ++r) t = __builtin_amdgcn_mfma_f64_16x16x4f64(v[r], v[r], t, 0, 0, 0);
 #pragma unroll
         for (int r = 0; r < 4; ++r) DTn[r * 64 + lane_o] = t[r];
         wave_lds_sync();
       }
       wave_lds_sync();
-      bad |= panel(DTn, BV + 16 * (k + 1), YV + 16 * (k + 1), lane_o);
-    } else if (k >= 0) {
+      if (!KO(3)) bad |= panel(DTn, BV + 16 * (k + 1), YV + 16 * (k + 1), lane_o);
+    } else if (k >= 0 && !KO(4)) {
       // b_b -= U_kb^T y_k for b >= k + 2: one output per lane of the other waves
       const int vt = ((wave_o - pw - 1 + NW) % NW) * 64 + lane_o;
       const int bq = k + 2 + (vt >> 4), c = vt & 15;
@@ -732,26 +749,30 @@ __device__ __forceinline__ bool factor_forward(const GnArgs& a, const SmemLayout
         BV[16 * bq + c] -= s0 + s1;
       }
     }
+    DIAG_MARK(12);
+    // off-diagonal trailing update over the slot suffix [sU, nS)
+    if (k >= 0 && !KO(1)) {
 #pragma unroll
-    for (int s = 0; s < SLOTS; ++s) {
-      const int IJ = slot_ij(stab_o, s);
-      const int I = IJ & 0xffff, J = IJ >> 16;
-      if (IJ >= 0 && J > k && k >= 0) {
-        const double* ua = PB + (J - k - 1) * 256 + lane_o;
-        const double* ub = PB + (I - k - 1) * 256 + lane_o;
-        double av[4], bv[4];
+      for (int s = 0; s < SLOTS; ++s) {
+        if (s >= sU && s < nS) {
+          const int IJ = slot_ij(stab_o, s);
+          const double* ua = PB + ((IJ >> 16) - k - 1) * 256 + lane_o;
+          const double* ub = PB + ((IJ & 0xffff) - k - 1) * 256 + lane_o;
+          double av[4], bv[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          av[r] = ua[64 * r];
-          bv[r] = ub[64 * r];
+          for (int r = 0; r < 4; ++r) {
+            av[r] = ua[64 * r];
+            bv[r] = ub[64 * r];
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[r], bv[r], acc[s], 0, 0, 0);
         }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(-av[r], bv[r], acc[s], 0, 0, 0);
       }
     }
+    DIAG_MARK(13);
     // remaining diagonal blocks J > k + 1 of this wave
     for (int J = wave_o; J < NT; J += NW) {
-      if (J <= k + 1 || k < 0) continue;
+      if (J <= k + 1 || k < 0 || KO(2)) continue;
       double* DTj = DT + J * DTS;
       d4 t;
       double v[4];
@@ -761,7 +782,7 @@ __device__ __forceinline__ bool factor_forward(const GnArgs& a, const SmemLayout
         v[r] = PB[(J - k - 1) * 256 + r * 64 + lane_o];
       }
 #pragma unroll
-      for (int r = 0; r < 4; ++r) t = __builtin_amdgcn_mfma_f64_16x16x4f64(-v[r], v[r], t, 0, 0, 0);
+      for (int r = 0; r < 4; ++r) t = __builtin_amdgcn_mfma_f64_16x16x4f64(v[r], v[r], t, 0, 0, 0);
 #pragma unroll
       for (int r = 0; r < 4; ++r) DTj[r * 64 + lane_o] = t[r];
     }
@@ -774,19 +795,37 @@ __device__ __forceinline__ bool factor_forward(const GnArgs& a, const SmemLayout
   return flag[0] == 0;
 }
 
-// delta_k = L_kk^-T y_k for lanes 0..15 (row lane of L^-T, y broadcast), in place.
+// Sum over the four 16-lane rows of a wave (v_permlane16/32_swap), result in every row.
+__device__ __forceinline__ double rows4_sum(double v) {
+  long long b = __double_as_longlong(v);
+  int lo = (int)b, hi = (int)(b >> 32);
+  auto l1 = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  auto h1 = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  v = __longlong_as_double(((long long)h1[0] << 32) | (unsigned int)l1[0]) +
+      __longlong_as_double(((long long)h1[1] << 32) | (unsigned int)l1[1]);
+  b = __double_as_longlong(v);
+  lo = (int)b;
+  hi = (int)(b >> 32);
+  auto l2 = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+  auto h2 = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+  return __longlong_as_double(((long long)h2[0] << 32) | (unsigned int)l2[0]) +
+         __longlong_as_double(((long long)h2[1] << 32) | (unsigned int)l2[1]);
+}
+
+// delta_k = L_kk^-T y_k, in place, by one whole wave: lane (c, g = l >> 4) sums
+// the four terms q = 4g..4g+3 of row c of L^-T, rows4_sum completes the dot.
 __device__ __forceinline__ void block_back(const double* LT, double* yv, int lane) {
-  if (lane < 16) {
-    double s0 = 0.0, s1 = 0.0;
-#pragma unroll
-    for (int q = 0; q < 16; q += 2) {
-      s0 += LT[lane * LIS + q] * yv[q];
-      s1 += LT[lane * LIS + q + 1] * yv[q + 1];
-    }
-    const double dv = s0 + s1;
-    wave_lds_sync();  // every lane has read y before any lane overwrites it
-    yv[lane] = dv;
-  }
+  const int c = lane & 15, g = lane >> 4;
+  const double2 y01 = *(const double2*)(yv + 4 * g);
+  const double2 y23 = *(const double2*)(yv + 4 * g + 2);
+  const double* lt = LT + c * LIS + 4 * g;
+  double s = lt[0] * y01.x;
+  s = fma(lt[1], y01.y, s);
+  s = fma(lt[2], y23.x, s);
+  s = fma(lt[3], y23.y, s);
+  const double dv = rows4_sum(s);
+  wave_lds_sync();  // every lane has read y before any lane overwrites it
+  if (lane < 16) yv[c] = dv;
 }
 
 // Backward solve U delta = y (YV, in place), right-looking over block columns:
@@ -803,7 +842,7 @@ __device__ __forceinline__ void backward(const GnArgs& a, const SmemLayout& SL, 
   if (wave == (NT - 1) % NW) block_back(DT + (NT - 1) * DTS, DV + 16 * (NT - 1), lane);
   __syncthreads();
 #pragma unroll 1
-  for (int bb = NT - 1; bb >= 1; --bb) {
+  for (int bb = NT - 1; bb >= 1 && !KO(5); --bb) {
     int lane_o = lane, stab_o = stab;
     asm volatile("" : "+v"(lane_o));
     asm volatile("" : "+v"(stab_o));
@@ -892,15 +931,15 @@ __global__ __launch_bounds__(NTHREADS, 2) void k_gn(GnArgs a) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int row = 16 * J + (lane >> 4) + 4 * r, col = 16 * I + (lane & 15);
-            Hb[(size_t)row * dp + col] = acc[s][r];
-            if (I != J) Hb[(size_t)col * dp + row] = acc[s][r];
+            Hb[(size_t)row * dp + col] = -acc[s][r];
+            if (I != J) Hb[(size_t)col * dp + row] = -acc[s][r];
           }
         }
       }
       __syncthreads();  // diagonal tiles (LDS) complete
       for (int t = threadIdx.x; t < a.NT * 256; t += NTHREADS) {
         const int J = t >> 8, tr = (t >> 4) & 15, tc = t & 15;
-        Hb[(size_t)(16 * J + tr) * dp + 16 * J + tc] = sm[SL.DT + J * DTS + (t & 255)];
+        Hb[(size_t)(16 * J + tr) * dp + 16 * J + tc] = -sm[SL.DT + J * DTS + (t & 255)];
       }
       for (int t = threadIdx.x; t < dp; t += NTHREADS) a.gout[(size_t)b * dp + t] = -sm[SL.BV + t];
       if (threadIdx.x == 0) a.cost[b] = c1;
