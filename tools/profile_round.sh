@@ -4,7 +4,7 @@
 set -e
 TAG=${1:-r01}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-B="python bench.py --steps 3 --warmup 1 --no-cpu"
+B="python bench.py --steps 10 --warmup 2 --no-cpu"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${TAG}_trace -o run -- $B > gpurun_out/prof_${TAG}_trace.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_${TAG}_fetch -o run -- $B > gpurun_out/prof_${TAG}_fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_${TAG}_write -o run -- $B > gpurun_out/prof_${TAG}_write.log 2>&1
