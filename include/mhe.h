@@ -149,6 +149,45 @@ int mhe_chol_solve(const mhe_dims* dims, const void* const_buf, int32_t batch,
                    const double* H, const double* g, double* delta, int32_t* status,
                    void* stream);
 
+/* ------------------------------------------------------------------------
+ * Batched extended Kalman filter.
+ * Replaces utils/ekf.py:20-61 (EKF.update / predict / correct) with the
+ * utils/gnss.py plug-ins, for `batch` independent filter instances, `steps`
+ * updates each, in one launch (one wavefront per instance).
+ * ------------------------------------------------------------------------ */
+#define MHE_EKF_DYN_GNSS_POS_AND_BIAS 1          /* utils/gnss.py:79-90 (n=5, m=3, params dt) */
+#define MHE_EKF_MEAS_MULTI_PSEUDORANGE 1         /* utils/gnss.py:27-45 (q=3: sat ENU position) */
+#define MHE_EKF_MEAS_MULTI_PSEUDORANGE_AND_BIAS 2 /* utils/gnss.py:48-61 (last row: bias, zero Jacobian row) */
+
+typedef struct mhe_ekf_dims {
+  int32_t n, m;        /* state and control sizes of the dynamics model */
+  int32_t pmax;        /* row capacity of Z / PAR / R per step (<= 32) */
+  int32_t q;           /* parameters per measurement row (3) */
+  int32_t dyn_model;   /* MHE_EKF_DYN_* */
+  int32_t meas_model;  /* MHE_EKF_MEAS_* */
+  double dt;           /* dyn_func_params["dt"] */
+} mhe_ekf_dims;
+
+/*
+ * All pointers are device pointers; a batch stride of 0 broadcasts one array to
+ * every instance.  Per instance b and step k:
+ *   U   (steps, m)                      at U   + b*u_bstride
+ *   Z   (steps, pmax), rows 0..nz-1     at Z   + b*z_bstride   (z, utils/ekf.py:20)
+ *   nz  (steps) valid rows; 0 = no measurement (predict only, utils/ekf.py:30-38)
+ *   PAR (steps, pmax, q)                at PAR + b*par_bstride (meas_func_params)
+ *   R   leading nz x nz block of (pmax, pmax) at R + b*r_bstride + k*r_sstride
+ *   Q   (n, n) shared.
+ * mu (B,n) and S (B,n,n) hold the prior on entry and the final state on exit;
+ * mu_hist (B,steps,n) / S_hist (B,steps,n,n) (optional) receive the state after
+ * every update; status (B, optional): 0 ok, 1 innovation covariance not SPD,
+ * 2 nz > 32.  Returns MHE_OK or a negative MHE_ERR_*.
+ */
+int mhe_ekf_run(const mhe_ekf_dims* dims, int32_t batch, int32_t steps, double* mu, double* S,
+                const double* U, int64_t u_bstride, const double* Z, int64_t z_bstride,
+                const int32_t* nz, int64_t nz_bstride, const double* PAR, int64_t par_bstride,
+                const double* Q, const double* R, int64_t r_bstride, int64_t r_sstride,
+                double* mu_hist, double* S_hist, int32_t* status, void* stream);
+
 /* Library version string. */
 const char* mhe_version(void);
 

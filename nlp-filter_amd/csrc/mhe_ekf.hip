@@ -1,0 +1,284 @@
+// libmhe: batched extended Kalman filter for MI355X (gfx950).
+//
+// Replaces utils/ekf.py:20-61 (EKF.update -> predict / correct, kingdwd/nlp-filter)
+// for many independent filter instances at once: ONE WAVEFRONT PER FILTER runs
+// all `steps` updates of its instance; four instances per workgroup.  Per step
+//   predict:  mu- = f(mu, u),  S- = G S G^T + Q                (utils/ekf.py:40-45)
+//   correct:  P = H S- H^T + R,  K = S- H^T P^-1,
+//             mu = mu- + K (z - h(mu-)),  S = S- - K H S-        (utils/ekf.py:47-61)
+// The reference forms P^-1 explicitly (utils/ekf.py:55).  Here one augmented
+// right-looking Cholesky sweep over [P | H S- | e] (row per lane, pivots and
+// L_jc broadcast by v_readlane) gives Y = L^-1 H S- and w = L^-1 e, so that
+//   K e = Y^T w   and   K H S- = Y^T Y
+// -- no inverse and no back substitution; S stays symmetric by construction.
+// Results agree with the reference to floating-point rounding (tests state the
+// tolerance).  Plug-ins are the utils/gnss.py models as device functors.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "mhe.h"
+
+namespace mhe_ekf {
+
+constexpr int NWF = 4;     // filters (waves) per workgroup
+constexpr int MAXP = 32;   // measurement rows per step (nz <= MAXP)
+
+// ---------------------------------------------------------------- plug-ins
+// gnss_pos_and_bias, utils/gnss.py:79-90: x+ = x + dt [u0, u1, u2, x4, 0],
+// G = I + dt e_3 e_4^T (the reference updates x in place; G does not depend on x).
+struct EkfGnssPosAndBias {
+  static constexpr int n = 5, m = 3;
+  __device__ static void step(const double* x, const double* u, double dt, double* xp, double* G) {
+    xp[0] = x[0] + dt * u[0];
+    xp[1] = x[1] + dt * u[1];
+    xp[2] = x[2] + dt * u[2];
+    xp[3] = x[3] + dt * x[4];
+    xp[4] = x[4] + dt * 0.0;
+    for (int i = 0; i < n * n; ++i) G[i] = 0.0;
+    for (int i = 0; i < n; ++i) G[i * n + i] = 1.0;
+    G[3 * n + 4] = dt;
+  }
+};
+
+// Row i of multi_pseudorange (utils/gnss.py:27-45 via pseudorange :4-24):
+//   h = |x[:3] - s_i| + x[3],  H = [-(s_i - x[:3]) / |s_i - x[:3]|, 1, 0]
+// with_bias (multi_pseudorange_and_bias, :48-61): the extra last row is h = x[3]
+// and -- bug-compatible -- an all-zero Jacobian row.
+template <bool with_bias>
+struct EkfMultiPseudorange {
+  static constexpr int q = 3;
+  template <int n>
+  __device__ static void row(const double* x, const double* par, int i, int nz, double& h, double* H) {
+    if (with_bias && i == nz - 1) {
+      h = x[3];
+      for (int c = 0; c < n; ++c) H[c] = 0.0;
+      return;
+    }
+    const double l0 = par[0] - x[0], l1 = par[1] - x[1], l2 = par[2] - x[2];
+    const double r = sqrt(l0 * l0 + l1 * l1 + l2 * l2);
+    h = sqrt((x[0] - par[0]) * (x[0] - par[0]) + (x[1] - par[1]) * (x[1] - par[1]) +
+             (x[2] - par[2]) * (x[2] - par[2])) + x[3];
+    for (int c = 0; c < n; ++c) H[c] = 0.0;
+    H[0] = -l0 / r;
+    H[1] = -l1 / r;
+    H[2] = -l2 / r;
+    H[3] = 1.0;
+  }
+};
+
+struct EkfArgs {
+  int batch, steps, nmeas_rows_max;
+  double dt;
+  double* mu;
+  double* S;
+  const double* U;
+  long long u_bstride;
+  const double* Z;
+  long long z_bstride;
+  const int* nz;
+  long long nz_bstride;
+  const double* PAR;
+  long long par_bstride;
+  const double* Q;
+  const double* R;
+  long long r_bstride, r_sstride;
+  double* mu_hist;
+  double* S_hist;
+  int* status;
+};
+
+__device__ __forceinline__ double readlane_d(double v, int lane) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)b, lane);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// per-wave LDS scratch (doubles)
+template <int n>
+struct WaveSmem {
+  static constexpr int MU = 0, S = MU + n, G = S + n * n, SP = G + n * n, MP = SP + n * n, H = MP + n,
+                       T1 = H + MAXP * n, E = T1 + MAXP * n, Y = E + MAXP, W = Y + MAXP * n, total = W + MAXP;
+};
+
+template <class DYN, class MEAS>
+__global__ __launch_bounds__(NWF * 64) void k_ekf(EkfArgs a) {
+  constexpr int n = DYN::n, m = DYN::m, q = MEAS::q;
+  using WS = WaveSmem<n>;
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int b = blockIdx.x * NWF + wave;
+  if (b >= a.batch) return;  // whole wave exits; no workgroup barrier is used below
+  double* sw = smem + wave * WS::total;
+  double* mu = sw + WS::MU;
+  double* S = sw + WS::S;
+  double* G = sw + WS::G;
+  double* SP = sw + WS::SP;
+  double* MP = sw + WS::MP;
+  double* H = sw + WS::H;
+  double* T1 = sw + WS::T1;
+  double* E = sw + WS::E;
+  double* Y = sw + WS::Y;
+  double* W = sw + WS::W;
+  for (int t = lane; t < n; t += 64) mu[t] = a.mu[(size_t)b * n + t];
+  for (int t = lane; t < n * n; t += 64) S[t] = a.S[(size_t)b * n * n + t];
+  int status = 0;
+  __builtin_amdgcn_wave_barrier();
+  for (int k = 0; k < a.steps; ++k) {
+    // ---- predict (utils/ekf.py:40-45)
+    if (lane == 0) {
+      double x[n], u[m > 0 ? m : 1], xp[n], Gl[n * n];
+      for (int c = 0; c < n; ++c) x[c] = mu[c];
+      const double* up = a.U + (long long)b * a.u_bstride + (long long)k * m;
+      for (int c = 0; c < m; ++c) u[c] = up[c];
+      DYN::step(x, u, a.dt, xp, Gl);
+      for (int c = 0; c < n; ++c) MP[c] = xp[c];
+      for (int c = 0; c < n * n; ++c) G[c] = Gl[c];
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    for (int t = lane; t < n * n; t += 64) {  // S- = G S G^T + Q
+      const int r = t / n, c = t % n;
+      double acc = 0.0;
+      for (int kk = 0; kk < n; ++kk) {
+        double gs = 0.0;
+        for (int l = 0; l < n; ++l) gs += S[kk * n + l] * G[c * n + l];  // (S G^T)[kk][c]
+        acc += G[r * n + kk] * gs;
+      }
+      SP[t] = acc + a.Q[t];
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    const int nz = a.nz[(long long)b * a.nz_bstride + k];
+    if (nz > 0 && nz <= MAXP) {
+      // ---- measurement rows at mu- (utils/ekf.py:51)
+      const double* zk = a.Z + (long long)b * a.z_bstride + (long long)k * a.nmeas_rows_max;
+      const double* pk = a.PAR + (long long)b * a.par_bstride + (long long)k * a.nmeas_rows_max * q;
+      if (lane < nz) {
+        double x[n], h, Hr[n];
+        for (int c = 0; c < n; ++c) x[c] = MP[c];
+        MEAS::template row<n>(x, pk + lane * q, lane, nz, h, Hr);
+        for (int c = 0; c < n; ++c) H[lane * n + c] = Hr[c];
+        E[lane] = zk[lane] - h;
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      for (int t = lane; t < nz * n; t += 64) {  // T1 = H S-
+        const int i = t / n, c = t % n;
+        double acc = 0.0;
+        for (int l = 0; l < n; ++l) acc += H[i * n + l] * SP[l * n + c];
+        T1[t] = acc;
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      // ---- augmented sweep: lane i holds row i of [P | T1 | e], P = T1 H^T + R
+      const double* Rk = a.R + (long long)b * a.r_bstride + (long long)k * a.r_sstride;
+      const int i = lane;
+      const bool row = i < nz;
+      double p[MAXP], t1[n], e = 0.0;
+#pragma unroll
+      for (int j = 0; j < MAXP; ++j) {
+        double acc = 0.0;
+        if (row && j < nz) {
+          for (int l = 0; l < n; ++l) acc += T1[i * n + l] * H[j * n + l];
+          acc += Rk[i * a.nmeas_rows_max + j];
+        }
+        p[j] = acc;
+      }
+#pragma unroll
+      for (int c = 0; c < n; ++c) t1[c] = row ? T1[i * n + c] : 0.0;
+      if (row) e = E[i];
+      double idg = 0.0;
+      bool bad = false;
+#pragma unroll
+      for (int c = 0; c < MAXP; ++c) {
+        if (c < nz) {
+          const double piv = readlane_d(p[c], c);
+          bad |= !(piv > 0.0 && piv < INFINITY);
+          const double rs = 1.0 / sqrt(piv);
+          const double qv = p[c] * rs;                 // L_ic (i > c)
+          const double mm = (i > c && row) ? qv * rs : 0.0;  // A'_ic / A'_cc
+          idg = (i == c) ? rs : idg;
+#pragma unroll
+          for (int j = c + 1; j < MAXP; ++j)
+            if (j < nz) p[j] -= qv * readlane_d(qv, j);
+#pragma unroll
+          for (int cc = 0; cc < n; ++cc) t1[cc] -= mm * readlane_d(t1[cc], c);
+          e -= mm * readlane_d(e, c);
+        }
+      }
+      if (bad) status = 1;
+      if (row) {
+#pragma unroll
+        for (int c = 0; c < n; ++c) Y[i * n + c] = t1[c] * idg;  // Y = L^-1 H S-
+        W[i] = e * idg;                                         // w = L^-1 e
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      // mu = mu- + Y^T w ; S = S- - Y^T Y   (utils/ekf.py:34-35, 58-59)
+      for (int t = lane; t < n * n; t += 64) {
+        const int r = t / n, c = t % n;
+        double acc = 0.0;
+        for (int ii = 0; ii < nz; ++ii) acc += Y[ii * n + r] * Y[ii * n + c];
+        S[t] = SP[t] - acc;
+      }
+      for (int t = lane; t < n; t += 64) {
+        double acc = 0.0;
+        for (int ii = 0; ii < nz; ++ii) acc += Y[ii * n + t] * W[ii];
+        mu[t] = MP[t] + acc;
+      }
+    } else {
+      if (nz > MAXP) status = 2;
+      for (int t = lane; t < n * n; t += 64) S[t] = SP[t];
+      for (int t = lane; t < n; t += 64) mu[t] = MP[t];
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    if (a.mu_hist)
+      for (int t = lane; t < n; t += 64) a.mu_hist[((size_t)b * a.steps + k) * n + t] = mu[t];
+    if (a.S_hist)
+      for (int t = lane; t < n * n; t += 64) a.S_hist[((size_t)b * a.steps + k) * n * n + t] = S[t];
+  }
+  for (int t = lane; t < n; t += 64) a.mu[(size_t)b * n + t] = mu[t];
+  for (int t = lane; t < n * n; t += 64) a.S[(size_t)b * n * n + t] = S[t];
+  if (a.status && lane == 0) a.status[b] = status;
+}
+
+template <class DYN, class MEAS>
+int launch(EkfArgs& a, hipStream_t st) {
+  const int smem = NWF * WaveSmem<DYN::n>::total * (int)sizeof(double);
+  hipLaunchKernelGGL((k_ekf<DYN, MEAS>), dim3((a.batch + NWF - 1) / NWF), dim3(NWF * 64), smem, st, a);
+  return hipGetLastError() == hipSuccess ? MHE_OK : MHE_ERR_HIP;
+}
+
+}  // namespace mhe_ekf
+
+extern "C" int mhe_ekf_run(const mhe_ekf_dims* dims, int32_t batch, int32_t steps, double* mu, double* S,
+                           const double* U, int64_t u_bstride, const double* Z, int64_t z_bstride, const int32_t* nz,
+                           int64_t nz_bstride, const double* PAR, int64_t par_bstride, const double* Q,
+                           const double* R, int64_t r_bstride, int64_t r_sstride, double* mu_hist, double* S_hist,
+                           int32_t* status, void* stream) {
+  using namespace mhe_ekf;
+  if (!dims) return MHE_ERR_NULL;
+  if (batch < 0 || steps < 0 || dims->pmax < 1 || dims->pmax > MAXP) return MHE_ERR_DIMS;
+  if (batch == 0 || steps == 0) return MHE_OK;
+  if (!mu || !S || !Q || !nz || !Z || !R || (dims->m > 0 && !U)) return MHE_ERR_NULL;
+  EkfArgs a = {};
+  a.batch = batch; a.steps = steps; a.nmeas_rows_max = dims->pmax; a.dt = dims->dt;
+  a.mu = mu; a.S = S; a.U = U; a.u_bstride = u_bstride; a.Z = Z; a.z_bstride = z_bstride; a.nz = nz;
+  a.nz_bstride = nz_bstride; a.PAR = PAR; a.par_bstride = par_bstride; a.Q = Q; a.R = R; a.r_bstride = r_bstride;
+  a.r_sstride = r_sstride; a.mu_hist = mu_hist; a.S_hist = S_hist; a.status = status;
+  hipStream_t st = (hipStream_t)stream;
+  if (dims->dyn_model != MHE_EKF_DYN_GNSS_POS_AND_BIAS || dims->n != 5 || dims->m != 3) return MHE_ERR_MODEL;
+  if (dims->q != 3) return MHE_ERR_DIMS;
+  if (!PAR) return MHE_ERR_NULL;
+  switch (dims->meas_model) {
+    case MHE_EKF_MEAS_MULTI_PSEUDORANGE:
+      return launch<EkfGnssPosAndBias, EkfMultiPseudorange<false>>(a, st);
+    case MHE_EKF_MEAS_MULTI_PSEUDORANGE_AND_BIAS:
+      return launch<EkfGnssPosAndBias, EkfMultiPseudorange<true>>(a, st);
+  }
+  return MHE_ERR_MODEL;
+}

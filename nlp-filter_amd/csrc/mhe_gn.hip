@@ -563,8 +563,9 @@ __device__ __forceinline__ void load_tiles(const GnArgs& a, const SmemLayout& SL
       const int I = IJ & 0xffff, J = IJ >> 16;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
+        // upper block (J, I) of the tile = transpose of the lower block read from H
         const int row = 16 * J + (lane >> 4) + 4 * r, col = 16 * I + (lane & 15);
-        acc[s][r] = -Hb[(size_t)row * dp + col];
+        acc[s][r] = -Hb[(size_t)col * dp + row];
       }
     }
   }

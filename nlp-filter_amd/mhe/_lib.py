@@ -27,7 +27,13 @@ class MheDims(ctypes.Structure):
     ]
 
 
+class MheEkfDims(ctypes.Structure):
+    _fields_ = [("n", c_i32), ("m", c_i32), ("pmax", c_i32), ("q", c_i32),
+                ("dyn_model", c_i32), ("meas_model", c_i32), ("dt", c_dbl)]
+
+
 _P = ctypes.POINTER(MheDims)
+_PE = ctypes.POINTER(MheEkfDims)
 SIGNATURES = {
     "mhe_version": (ctypes.c_char_p, []),
     "mhe_padded_dim": (c_i32, [_P]),
@@ -38,6 +44,8 @@ SIGNATURES = {
     "mhe_assemble": (ctypes.c_int, [_P, c_vp, c_i32, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp,
                                     c_vp, c_vp, c_vp, c_vp]),
     "mhe_chol_solve": (ctypes.c_int, [_P, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "mhe_ekf_run": (ctypes.c_int, [_PE, c_i32, c_i32, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64,
+                                   c_vp, c_i64, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
 }
 
 

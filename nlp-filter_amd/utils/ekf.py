@@ -1,0 +1,136 @@
+"""Extended Kalman filter on the GPU -- drop-in for kingdwd/nlp-filter utils/ekf.py.
+
+``EKF(dyn_func, meas_func, mu0, S0)`` and ``EKF.update(u, z, Q, R,
+dyn_func_params, meas_func, meas_func_params)`` keep the reference signatures
+and semantics (utils/ekf.py:11-38): ``mu`` / ``S`` are NumPy arrays replaced by
+each update; ``z=None`` predicts only.  Each update is one launch of
+``mhe_ekf_run`` (csrc/mhe_ekf.hip); ``run_batch`` runs many independent filter
+instances over many steps in a single launch (the GPU-shaped entry point).
+Plug-ins are resolved by name (``utils.gnss.EKF_DYN`` / ``EKF_MEAS``); an
+unregistered plug-in raises ``UnsupportedPlugin`` -- there is no CPU path.
+
+Numerics: the reference forms inv(P) (utils/ekf.py:55); the kernel uses a
+Cholesky sweep of P, so results agree to floating-point rounding (tests state
+the tolerance).
+"""
+import ctypes
+
+import numpy as np
+
+from mhe import _lib
+from mhe.registry import UnsupportedPlugin
+
+from . import gnss as _gnss
+
+MAXP = 32
+
+
+def _name(fn):
+    return fn if isinstance(fn, str) else getattr(fn, "__name__", None)
+
+
+def models(dyn_func, meas_func):
+    dn, mn = _name(dyn_func), _name(meas_func)
+    if dn not in _gnss.EKF_DYN:
+        raise UnsupportedPlugin(f"EKF dynamics plug-in {dn!r} has no HIP functor; registered: {sorted(_gnss.EKF_DYN)}")
+    if mn not in _gnss.EKF_MEAS:
+        raise UnsupportedPlugin(f"EKF measurement plug-in {mn!r} has no HIP functor; registered: {sorted(_gnss.EKF_MEAS)}")
+    return _gnss.EKF_DYN[dn], _gnss.EKF_MEAS[mn]
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def run_batch(dyn_func, meas_func, mu0, S0, U, Z, nz, Q, R, dt, sat_pos, device=None, stream=None,
+              keep_history=True):
+    """Run B independent filters for T steps in one launch.
+
+    mu0 (B,n), S0 (B,n,n), U (B,T,m), Z (B,T,pmax), nz (B,T) valid rows per step
+    (0 = predict only), Q (n,n), R (T,pmax,pmax) or (B,T,pmax,pmax), sat_pos
+    (B,T,pmax,3); dt = dyn_func_params["dt"].  Inputs may be NumPy or torch.
+    Returns (mu_hist (B,T,n), S_hist (B,T,n,n), mu (B,n), S (B,n,n), status (B))
+    as torch tensors on the device."""
+    import torch
+
+    (did, n, m), (mid, _, q) = models(dyn_func, meas_func)
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+
+    def d(a, dt_=torch.float64):
+        return torch.as_tensor(np.asarray(a) if not torch.is_tensor(a) else a, dtype=dt_, device=dev).contiguous()
+
+    mu = d(mu0).clone()
+    S = d(S0).clone()
+    B = mu.shape[0]
+    Zt = d(Z)
+    T, pmax = Zt.shape[1], Zt.shape[2]
+    if pmax > MAXP:
+        raise ValueError(f"at most {MAXP} measurement rows per step")
+    Ut = d(U)
+    nzt = d(nz, torch.int32)
+    Pt = d(sat_pos)
+    Rt = d(R)
+    Qt = d(Q)
+    if mu.shape != (B, n) or S.shape != (B, n, n) or Ut.shape != (B, T, m) or nzt.shape != (B, T) \
+            or Pt.shape != (B, T, pmax, q) or Qt.shape != (n, n):
+        raise ValueError("run_batch: inconsistent shapes")
+    if Rt.dim() == 3:
+        r_b, r_s = 0, pmax * pmax
+        if Rt.shape != (T, pmax, pmax):
+            raise ValueError("R must be (T,pmax,pmax) or (B,T,pmax,pmax)")
+    else:
+        r_b, r_s = T * pmax * pmax, pmax * pmax
+        if Rt.shape != (B, T, pmax, pmax):
+            raise ValueError("R must be (T,pmax,pmax) or (B,T,pmax,pmax)")
+    mh = torch.empty((B, T, n), dtype=torch.float64, device=dev) if keep_history else None
+    Sh = torch.empty((B, T, n, n), dtype=torch.float64, device=dev) if keep_history else None
+    st = torch.empty(B, dtype=torch.int32, device=dev)
+    dims = _lib.MheEkfDims(n=n, m=m, pmax=pmax, q=q, dyn_model=did, meas_model=mid, dt=float(dt))
+    lib = _lib.load()
+    sh = stream.cuda_stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
+    rc = lib.mhe_ekf_run(ctypes.byref(dims), B, T, _ptr(mu), _ptr(S), _ptr(Ut), T * m, _ptr(Zt), T * pmax,
+                         _ptr(nzt), T, _ptr(Pt), T * pmax * q, _ptr(Qt), _ptr(Rt), r_b, r_s, _ptr(mh), _ptr(Sh),
+                         _ptr(st), ctypes.c_void_p(sh))
+    _lib.check(rc, "mhe_ekf_run")
+    return mh, Sh, mu, S, st
+
+
+class EKF(object):
+    """utils/ekf.py:4-18 -- notation of Probabilistic Robotics (Thrun et al.)."""
+
+    def __init__(self, dyn_func, meas_func, mu0, S0):
+        self.mu = mu0
+        self.S = S0
+        self.dynamics = dyn_func
+        self.measurement = meas_func
+        models(dyn_func, meas_func)  # fail at construction for unregistered plug-ins
+
+    def update(self, u, z, Q, R, dyn_func_params=None, meas_func=None, meas_func_params=None):
+        """One predict (+ correct when z is given) step, utils/ekf.py:20-38."""
+        meas = meas_func if meas_func is not None else self.measurement
+        (_, n, m), (_, extra, q) = models(self.dynamics, meas)
+        dt = float((dyn_func_params or {})["dt"])
+        mu0 = np.asarray(self.mu, dtype=np.float64).reshape(1, n)
+        S0 = np.asarray(self.S, dtype=np.float64).reshape(1, n, n)
+        u_ = np.asarray(u, dtype=np.float64).reshape(1, 1, m)
+        if z is None:
+            pmax, nz = 1, 0
+            Z = np.zeros((1, 1, 1))
+            P = np.zeros((1, 1, 1, q))
+            Rm = np.zeros((1, 1, 1))
+        else:
+            zz = np.atleast_1d(np.asarray(z, dtype=np.float64))
+            nz = pmax = zz.shape[0]
+            Z = zz.reshape(1, 1, pmax)
+            sp = np.asarray(meas_func_params["sat_pos"], dtype=np.float64).reshape(-1, q)
+            if sp.shape[0] + extra != nz:
+                raise ValueError("z and meas_func_params['sat_pos'] disagree in size")
+            P = np.zeros((1, 1, pmax, q))
+            P[0, 0, :sp.shape[0]] = sp
+            Rm = np.asarray(R, dtype=np.float64).reshape(1, pmax, pmax)
+        _, _, mu, S, st = run_batch(self.dynamics, meas, mu0, S0, u_, Z, np.full((1, 1), nz, np.int32),
+                                    np.asarray(Q, dtype=np.float64), Rm, dt, P, keep_history=False)
+        if int(st[0].item()) != 0:
+            raise np.linalg.LinAlgError("innovation covariance is not positive definite")
+        self.mu = mu[0].cpu().numpy()
+        self.S = S[0].cpu().numpy()
