@@ -126,8 +126,34 @@ int mhe_gn_solve(const mhe_dims* dims, const void* const_buf, int32_t batch,
                  double* cost_out, int32_t* iters_out, int32_t* status_out,
                  int32_t max_iter, double tol, void* stream);
 
-/* Padded system size used by the kernels: 16 * ceil(P*n / 16). */
+/* Padded system size used by the kernels: 16 * ceil(P*n / 16) on the
+ * register-resident path (<= 208); n * 16 * ceil(P / 16) (component-major
+ * ordering) on the large-system path. */
 int32_t mhe_padded_dim(const mhe_dims* dims);
+
+/*
+ * Workspace the large-system path needs for `batch` trajectories (bytes; 0 when
+ * the problem fits the register-resident kernel, which needs none).  Holds the
+ * per-trajectory H tiles, L_kk^-T blocks and iteration scratch.
+ */
+size_t mhe_workspace_bytes(const mhe_dims* dims, int32_t batch);
+
+/*
+ * mhe_gn_solve with a caller-owned device workspace of >= mhe_workspace_bytes
+ * (required when the padded system exceeds the register-resident limit: C3-C5,
+ * d = 1005 / 3006 / 8040).  Same arguments and results as mhe_gn_solve, which is
+ * this call with workspace = NULL (and returns MHE_ERR_NULL for such problems).
+ * Enqueues max_iter iterations of stream-ordered kernels; trajectories that
+ * converge or fail are frozen on the device, so no host synchronisation occurs.
+ */
+int mhe_gn_solve_ws(const mhe_dims* dims, const void* const_buf, int32_t batch,
+                    const double* X0, double* X_out,
+                    const double* U, int64_t u_bstride,
+                    const double* Y, const double* PAR, int64_t par_bstride,
+                    const double* x0,
+                    double* cost_out, int32_t* iters_out, int32_t* status_out,
+                    int32_t max_iter, double tol, void* workspace, size_t workspace_bytes,
+                    void* stream);
 
 /*
  * Kernel-level parity: assemble the GN normal equations at X.

@@ -1,0 +1,574 @@
+// libmhe: large-system Gauss-Newton path (padded system beyond the register-
+// resident limit, i.e. C3-C5: d = 1005 / 3006 / 8040).  Included by mhe_gn.hip
+// inside namespace mhe; shares the model functors and the panel / reduction
+// helpers with the register-resident kernel.
+//
+// Same iteration as k_gn (nlp/nlp.py:202-286 objective, GN with W eliminated),
+// run as a stream-ordered sequence of kernels per iteration over a caller-owned
+// workspace:
+//   k_big_resid    residuals, dynamics Jacobians, epoch-grouped measurement
+//                  terms G_e = sum_{i in e} H_i^T R_i H_i, gradient, cost
+//   k_big_assemble lower tiles of H in COMPONENT-MAJOR order (index a*Pp + j):
+//                  the (a,b) block is the P x P matrix
+//                    a^2 Qw_ab (D^T C D) - a (D^T diag(E_ab) + diag(E_ba) D)
+//                    + diag(FtE_ab) + Phi_E^T diag(G_ab) Phi_E
+//                  whose measurement part is an MFMA GEMM over the epochs
+//   k_big_chol     blocked right-looking Cholesky on HBM-resident 16x16 tiles
+//                  (diagonal blocks through the same single-wave panel as k_gn,
+//                  MFMA TRSM and trailing updates, block column cached in LDS
+//                  when it fits) + forward and backward solves
+//   k_big_update   X += delta (back to node-major), convergence / status
+// Converged or failed trajectories are frozen by a per-trajectory state word,
+// so the host loop only enqueues (no synchronisation).
+
+constexpr int BIG_NW = 8;
+constexpr int BIG_NTHREADS = BIG_NW * 64;
+constexpr int BIG_RUNNING = -1;
+
+__host__ __device__ inline int big_pp(int P) { return 16 * ((P + 15) / 16); }
+
+struct BigConst {  // byte offsets into the constants buffer
+  size_t D, Dt, DCD, cw, Qw, Pw, Rw, PhiE, PhiET, erow, ne, flag, total;
+};
+
+__host__ __device__ inline BigConst big_const_layout(int P, int M, int n, int p) {
+  BigConst L;
+  size_t o = 0;
+  const int Mr = M > 0 ? M : 1;
+  L.D = o;     o = align256(o + sizeof(double) * P * P);
+  L.Dt = o;    o = align256(o + sizeof(double) * P * P);
+  L.DCD = o;   o = align256(o + sizeof(double) * P * P);
+  L.cw = o;    o = align256(o + sizeof(double) * P);
+  L.Qw = o;    o = align256(o + sizeof(double) * n * n);
+  L.Pw = o;    o = align256(o + sizeof(double) * n * n);
+  L.Rw = o;    o = align256(o + sizeof(double) * Mr * p * p);
+  L.PhiE = o;  o = align256(o + sizeof(double) * Mr * P);   // unique measurement rows (epochs) x P
+  L.PhiET = o; o = align256(o + sizeof(double) * P * Mr);   // P x E (stride Mr)
+  L.erow = o;  o = align256(o + sizeof(int) * (Mr + 1));    // first row of each epoch, erow[E] = M
+  L.ne = o;    o = align256(o + sizeof(int));               // E
+  L.flag = o;  o = align256(o + sizeof(int) * Mr);          // scratch: row starts a new epoch
+  L.total = o;
+  return L;
+}
+
+struct BigWs {  // per-trajectory workspace offsets in doubles
+  size_t H, LT, BV, YV, XE, GEe, Ge, Es, FtE, Vs, FtV, total;
+};
+
+__host__ __device__ inline BigWs big_ws_layout(int P, int M, int n, int NT) {
+  BigWs W;
+  size_t o = 0;
+  const size_t ntiles = (size_t)NT * (NT + 1) / 2;
+  const int Mr = M > 0 ? M : 1;
+  const int dp = 16 * NT;
+  auto al = [](size_t x) { return (x + 31) & ~size_t(31); };  // 256-B alignment
+  W.H = o;   o = al(o + ntiles * 256);
+  W.LT = o;  o = al(o + (size_t)NT * DTS);
+  W.BV = o;  o = al(o + dp);
+  W.YV = o;  o = al(o + dp);
+  W.XE = o;  o = al(o + (size_t)Mr * n);
+  W.GEe = o; o = al(o + (size_t)Mr * n);
+  W.Ge = o;  o = al(o + (size_t)Mr * n * n);
+  W.Es = o;  o = al(o + (size_t)P * n * n);
+  W.FtE = o; o = al(o + (size_t)P * n * n);
+  W.Vs = o;  o = al(o + (size_t)P * n);
+  W.FtV = o; o = al(o + (size_t)P * n);
+  W.total = o;
+  return W;
+}
+
+struct BigArgs {
+  const char* cbuf;
+  int P, M, n, Pp, NTc, NT, q, has_prior;
+  int idx[8];
+  double alpha;
+  const double* U;
+  long long ustride;
+  const double* Y;
+  const double* PAR;
+  long long pstride;
+  const double* x0;
+  double* X;       // (B, P, n) current iterate (X_out)
+  double* cost;
+  int* iters;
+  int* state;      // BIG_RUNNING or final MHE_STATUS_*
+  double tol;
+  double* ws;      // workspace base
+  size_t ws_stride;  // doubles per trajectory
+  int cache_tiles;   // block-column tiles cached in LDS by k_big_chol
+};
+
+__device__ __forceinline__ int big_tile_index(int I, int J, int NT) { return J * NT - J * (J - 1) / 2 + (I - J); }
+
+// ------------------------------------------------------------ residuals
+template <class DYN, class MEAS>
+__global__ __launch_bounds__(BIG_NTHREADS) void k_big_resid(BigArgs a, int final_pass) {
+  constexpr int n = DYN::n, m = DYN::m, p = MEAS::p, q = MEAS::q;
+  const int b = blockIdx.x;
+  if (!final_pass && a.state[b] != BIG_RUNNING) return;
+  const BigConst CL = big_const_layout(a.P, a.M, n, p);
+  const BigWs WL = big_ws_layout(a.P, a.M, n, a.NT);
+  double* ws = a.ws + (size_t)b * a.ws_stride;
+  const double* D = (const double*)(a.cbuf + CL.D);
+  const double* Dt = (const double*)(a.cbuf + CL.Dt);
+  const double* cw = (const double*)(a.cbuf + CL.cw);
+  const double* Qw = (const double*)(a.cbuf + CL.Qw);
+  const double* Pw = (const double*)(a.cbuf + CL.Pw);
+  const double* Rw = (const double*)(a.cbuf + CL.Rw);
+  const double* PhiE = (const double*)(a.cbuf + CL.PhiE);
+  const double* PhiET = (const double*)(a.cbuf + CL.PhiET);
+  const int* erow = (const int*)(a.cbuf + CL.erow);
+  const int E = a.M > 0 ? *(const int*)(a.cbuf + CL.ne) : 0;
+  const int Mr = a.M > 0 ? a.M : 1;
+  const double* X = a.X + (size_t)b * a.P * n;
+  __shared__ double red[BIG_NW];
+  double cost = 0.0;
+  // interpolated states at the epochs: x_e = sum_j Phi_E[e][j] X_j
+  for (int e = threadIdx.x; e < E; e += BIG_NTHREADS) {
+    double xe[n];
+    for (int c = 0; c < n; ++c) xe[c] = 0.0;
+    for (int j = 0; j < a.P; ++j) {
+      const double ph = PhiET[(size_t)j * Mr + e];
+      for (int c = 0; c < n; ++c) xe[c] += ph * X[j * n + c];
+    }
+    for (int c = 0; c < n; ++c) ws[WL.XE + e * n + c] = xe[c];
+  }
+  // nodes (nlp/nlp.py:225-245)
+  for (int k = threadIdx.x; k < a.P; k += BIG_NTHREADS) {
+    double dx[n], xk[n], uk[m > 0 ? m : 1], f[n], F[n * n];
+    for (int c = 0; c < n; ++c) dx[c] = 0.0;
+    for (int j = 0; j < a.P; ++j) {
+      const double dv = Dt[(size_t)j * a.P + k];
+      for (int c = 0; c < n; ++c) dx[c] += dv * X[j * n + c];
+    }
+    for (int c = 0; c < n; ++c) xk[c] = X[k * n + c];
+    if (m > 0) {
+      const double* Up = a.U + (long long)b * a.ustride + (long long)k * m;
+      for (int c = 0; c < m; ++c) uk[c] = Up[c];
+    }
+    DYN::eval(xk, uk, f, F);
+    double W[n], V[n];
+    for (int c = 0; c < n; ++c) W[c] = a.alpha * dx[c] - f[c];
+    const double ck = cw[k];
+    for (int r = 0; r < n; ++r) {
+      double s = 0.0;
+      for (int c = 0; c < n; ++c) s += Qw[r * n + c] * W[c];
+      V[r] = ck * s;
+      cost += W[r] * V[r];
+    }
+    for (int r = 0; r < n; ++r) {
+      ws[WL.Vs + k * n + r] = V[r];
+      double s = 0.0;
+      for (int t = 0; t < n; ++t) s += F[t * n + r] * V[t];
+      ws[WL.FtV + k * n + r] = s;
+      for (int c = 0; c < n; ++c) {
+        double e = 0.0;
+        for (int t = 0; t < n; ++t) e += Qw[r * n + t] * F[t * n + c];
+        ws[WL.Es + (k * n + r) * n + c] = ck * e;
+      }
+    }
+    for (int r = 0; r < n; ++r)
+      for (int c = 0; c < n; ++c) {
+        double u = 0.0;
+        for (int t = 0; t < n; ++t) {
+          double e = 0.0;
+          for (int s2 = 0; s2 < n; ++s2) e += Qw[t * n + s2] * F[s2 * n + c];
+          u += F[t * n + r] * ck * e;
+        }
+        ws[WL.FtE + (k * n + r) * n + c] = u;
+      }
+  }
+  __syncthreads();
+  // measurement rows grouped by epoch (nlp/nlp.py:264-273)
+  for (int e = threadIdx.x; e < E; e += BIG_NTHREADS) {
+    double xe[n], ge[n], G[n * n];
+    for (int c = 0; c < n; ++c) {
+      xe[c] = ws[WL.XE + e * n + c];
+      ge[c] = 0.0;
+    }
+    for (int c = 0; c < n * n; ++c) G[c] = 0.0;
+    for (int i = erow[e]; i < erow[e + 1]; ++i) {
+      double par[q > 0 ? q : 1];
+      if (q > 0) {
+        const double* PR = a.PAR + (long long)b * a.pstride + (long long)i * q;
+        for (int c = 0; c < q; ++c) par[c] = PR[c];
+      }
+      double h[p], Hm[p * n];
+      MEAS::eval(xe, par, a.idx, h, Hm);
+      const double* yi = a.Y + ((long long)b * a.M + i) * p;
+      const double* R = Rw + (size_t)i * p * p;
+      double ev[p], Re[p];
+      for (int r = 0; r < p; ++r) ev[r] = yi[r] - h[r];
+      for (int r = 0; r < p; ++r) {
+        double s = 0.0;
+        for (int c = 0; c < p; ++c) s += R[r * p + c] * ev[c];
+        Re[r] = s;
+        cost += ev[r] * s;
+      }
+      for (int c = 0; c < n; ++c) {
+        double s = 0.0;
+        for (int r = 0; r < p; ++r) s += Hm[r * n + c] * Re[r];
+        ge[c] += s;
+      }
+      for (int r = 0; r < n; ++r)
+        for (int c = 0; c < n; ++c) {
+          double s = 0.0;
+          for (int t = 0; t < p; ++t) {
+            double rh = 0.0;
+            for (int t2 = 0; t2 < p; ++t2) rh += R[t * p + t2] * Hm[t2 * n + c];
+            s += Hm[t * n + r] * rh;
+          }
+          G[r * n + c] += s;
+        }
+    }
+    for (int c = 0; c < n; ++c) ws[WL.GEe + e * n + c] = ge[c];
+    for (int c = 0; c < n * n; ++c) ws[WL.Ge + e * n * n + c] = G[c];
+  }
+  __syncthreads();
+  // gradient, component-major: BV[a*Pp + j] = -g_(j,a)
+  for (int t = threadIdx.x; t < n * a.Pp; t += BIG_NTHREADS) {
+    const int c = t / a.Pp, j = t % a.Pp;
+    double gv = 0.0;
+    if (j < a.P) {
+      double s = 0.0;
+      for (int k = 0; k < a.P; ++k) s += D[(size_t)k * a.P + j] * ws[WL.Vs + k * n + c];
+      double o = 0.0;
+      for (int e = 0; e < E; ++e) o += PhiE[(size_t)e * a.P + j] * ws[WL.GEe + e * n + c];
+      gv = a.alpha * s - ws[WL.FtV + j * n + c] - o;
+      if (a.has_prior && j == 0) {
+        double t2 = 0.0;
+        for (int cc = 0; cc < n; ++cc) t2 += Pw[c * n + cc] * (X[cc] - a.x0[(long long)b * n + cc]);
+        gv += t2;
+      }
+    }
+    ws[WL.BV + t] = -gv;
+  }
+  if (a.has_prior && threadIdx.x == 0) {
+    for (int r = 0; r < n; ++r) {
+      double t2 = 0.0;
+      for (int c = 0; c < n; ++c) t2 += Pw[r * n + c] * (X[c] - a.x0[(long long)b * n + c]);
+      cost += (X[r] - a.x0[(long long)b * n + r]) * t2;
+    }
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  cost = wave_sum(cost);
+  if (lane == 0) red[wave] = cost;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double c = 0.0;
+    for (int w = 0; w < BIG_NW; ++w) c += red[w];
+    a.cost[b] = c;
+  }
+}
+
+// ------------------------------------------------------------ assembly
+// One wave per tile; grid (tiles / 4 per block, B).
+template <class DYN, class MEAS>
+__global__ __launch_bounds__(256) void k_big_assemble(BigArgs a) {
+  constexpr int n = DYN::n, p = MEAS::p;
+  const int b = blockIdx.y;
+  if (a.state[b] != BIG_RUNNING) return;
+  const BigConst CL = big_const_layout(a.P, a.M, n, p);
+  const BigWs WL = big_ws_layout(a.P, a.M, n, a.NT);
+  const double* ws = a.ws + (size_t)b * a.ws_stride;
+  double* H = a.ws + (size_t)b * a.ws_stride + WL.H;
+  const double* D = (const double*)(a.cbuf + CL.D);
+  const double* DCD = (const double*)(a.cbuf + CL.DCD);
+  const double* Qw = (const double*)(a.cbuf + CL.Qw);
+  const double* Pw = (const double*)(a.cbuf + CL.Pw);
+  const double* PhiE = (const double*)(a.cbuf + CL.PhiE);
+  const int E = a.M > 0 ? *(const int*)(a.cbuf + CL.ne) : 0;
+  const int lane = threadIdx.x & 63;
+  const int ntiles = a.NT * (a.NT + 1) / 2;
+  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= ntiles) return;
+  int J = 0, base = 0;
+  while (t >= base + (a.NT - J)) {
+    base += a.NT - J;
+    ++J;
+  }
+  const int I = J + (t - base);
+  const int ca = I / a.NTc, it = I % a.NTc, cb = J / a.NTc, jt = J % a.NTc;
+  // measurement part: sum_e Phi_E[e][j] G_e[ca][cb] Phi_E[e][l], MFMA over epochs
+  d4 acc = {0.0, 0.0, 0.0, 0.0};
+  {
+    const int jr = 16 * it + (lane & 15), lc = 16 * jt + (lane & 15);
+    for (int e0 = 0; e0 < E; e0 += 4) {
+      const int e = e0 + (lane >> 4);
+      double av = 0.0, bv = 0.0;
+      if (e < E) {
+        const double g = ws[WL.Ge + (size_t)e * n * n + ca * n + cb];
+        av = jr < a.P ? PhiE[(size_t)e * a.P + jr] * g : 0.0;
+        bv = lc < a.P ? PhiE[(size_t)e * a.P + lc] : 0.0;
+      }
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+    }
+  }
+  double* tile = H + (size_t)t * 256;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int tr = (lane >> 4) + 4 * r, tc = lane & 15;
+    const int j = 16 * it + tr, l = 16 * jt + tc;
+    double v;
+    if (j < a.P && l < a.P) {
+      v = acc[r] + a.alpha * a.alpha * Qw[ca * n + cb] * DCD[(size_t)j * a.P + l] -
+          a.alpha * (D[(size_t)l * a.P + j] * ws[WL.Es + (l * n + ca) * n + cb] +
+                     D[(size_t)j * a.P + l] * ws[WL.Es + (j * n + cb) * n + ca]);
+      if (j == l) v += ws[WL.FtE + (j * n + ca) * n + cb];
+      if (a.has_prior && j == 0 && l == 0) v += Pw[ca * n + cb];
+    } else {
+      v = (I == J && tr == tc) ? 1.0 : 0.0;
+    }
+    tile[tr * 16 + tc] = v;
+  }
+}
+
+// ------------------------------------------------------------ factor + solve
+__global__ __launch_bounds__(BIG_NTHREADS) void k_big_chol(BigArgs a) {
+  const int b = blockIdx.x;
+  if (a.state[b] != BIG_RUNNING) return;
+  const BigWs WL = big_ws_layout(a.P, a.M, a.n, a.NT);
+  double* ws = a.ws + (size_t)b * a.ws_stride;
+  double* H = ws + WL.H;
+  double* LTg = ws + WL.LT;
+  double* BV = ws + WL.BV;
+  double* YV = ws + WL.YV;
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  double* DT = sm;                 // DTS: -A_kk, then L_kk^-T
+  double* PART = sm + DTS;         // BIG_NW x 16 partial sums (backward)
+  double* YL = PART + BIG_NW * 16; // 16: block right-hand side (backward)
+  int* flag = (int*)(YL + 16);
+  double* PC = sm + DTS + BIG_NW * 16 + 16 + 2;  // cached block column, column-major tiles
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int NT = a.NT;
+  if (threadIdx.x == 0) *flag = 0;
+  for (int k = 0; k < NT; ++k) {
+    if (wave == 0) {
+      const double* Akk = H + (size_t)big_tile_index(k, k, NT) * 256;
+      for (int e = lane; e < 256; e += 64) DT[e] = -Akk[e];
+      wave_lds_sync();
+      const bool bad = panel(DT, BV + 16 * k, YV + 16 * k, lane);
+      if (bad && lane == 0) *flag = 1;
+      wave_lds_sync();
+      for (int e = lane; e < DTS; e += 64) LTg[(size_t)k * DTS + e] = DT[e];
+    }
+    __syncthreads();
+    if (*flag) break;
+    const bool cached = (NT - 1 - k) <= a.cache_tiles;
+    // TRSM: L_Ik = A_Ik L_kk^-T, I > k; b_I -= L_Ik y_k
+    for (int I = k + 1 + wave; I < NT; I += BIG_NW) {
+      double* Ak = H + (size_t)big_tile_index(I, k, NT) * 256;
+      double av[4], bv[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        av[r] = Ak[(lane & 15) * 16 + 4 * r + (lane >> 4)];
+        bv[r] = DT[(4 * r + (lane >> 4)) * LIS + (lane & 15)];
+      }
+      d4 u = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) u = __builtin_amdgcn_mfma_f64_16x16x4f64(av[r], bv[r], u, 0, 0, 0);
+      const double yc = YV[16 * k + (lane & 15)];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int tr = (lane >> 4) + 4 * r, tc = lane & 15;
+        Ak[tr * 16 + tc] = u[r];
+        if (cached) PC[(size_t)(I - k - 1) * 256 + tc * 16 + tr] = u[r];
+        const double s = row16_sum(u[r] * yc);
+        if ((lane & 15) == r) BV[16 * I + tr] -= s;
+      }
+    }
+    __syncthreads();
+    // trailing update A_IJ -= L_Ik L_Jk^T, k < J <= I
+    const int m = NT - 1 - k;
+    const int npairs = m * (m + 1) / 2;
+    for (int t = wave; t < npairs; t += BIG_NW) {
+      int jj = 0, base = 0;
+      while (t >= base + (m - jj)) {
+        base += m - jj;
+        ++jj;
+      }
+      const int J = k + 1 + jj, I = J + (t - base);
+      double* C = H + (size_t)big_tile_index(I, J, NT) * 256;
+      d4 c;
+      double av[4], bv[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        c[r] = C[((lane >> 4) + 4 * r) * 16 + (lane & 15)];
+        const int kk = 4 * r + (lane >> 4), mm = lane & 15;
+        if (cached) {
+          av[r] = -PC[(size_t)(I - k - 1) * 256 + kk * 16 + mm];
+          bv[r] = PC[(size_t)(J - k - 1) * 256 + kk * 16 + mm];
+        } else {
+          av[r] = -H[(size_t)big_tile_index(I, k, NT) * 256 + mm * 16 + kk];
+          bv[r] = H[(size_t)big_tile_index(J, k, NT) * 256 + mm * 16 + kk];
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) c = __builtin_amdgcn_mfma_f64_16x16x4f64(av[r], bv[r], c, 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) C[((lane >> 4) + 4 * r) * 16 + (lane & 15)] = c[r];
+    }
+    __syncthreads();
+  }
+  if (*flag) {
+    if (threadIdx.x == 0) a.state[b] = MHE_STATUS_NOT_SPD;
+    return;
+  }
+  // backward: delta_k = L_kk^-T (y_k - sum_{I>k} L_Ik^T delta_I), delta in place in YV
+  for (int k = NT - 1; k >= 0; --k) {
+    double pv = 0.0;
+    for (int I = k + 1 + wave; I < NT; I += BIG_NW) {
+      const double* L = H + (size_t)big_tile_index(I, k, NT) * 256;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int tr = (lane >> 4) + 4 * r;
+        pv += L[tr * 16 + (lane & 15)] * YV[16 * I + tr];
+      }
+    }
+    pv += __shfl_xor(pv, 16);
+    pv += __shfl_xor(pv, 32);
+    if (lane < 16) PART[wave * 16 + lane] = pv;
+    __syncthreads();
+    if (wave == 0) {
+      if (lane < 16) {
+        double rhs = YV[16 * k + lane];
+        for (int w = 0; w < BIG_NW; ++w) rhs -= PART[w * 16 + lane];
+        YL[lane] = rhs;
+      }
+      for (int e = lane; e < DTS; e += 64) DT[e] = LTg[(size_t)k * DTS + e];
+      wave_lds_sync();
+      block_back(DT, YL, lane);
+      wave_lds_sync();
+      if (lane < 16) YV[16 * k + lane] = YL[lane];
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------ update
+template <int n>
+__global__ __launch_bounds__(256) void k_big_update(BigArgs a) {
+  const int b = blockIdx.x;
+  if (a.state[b] != BIG_RUNNING) return;
+  const BigWs WL = big_ws_layout(a.P, a.M, n, a.NT);
+  const double* YV = a.ws + (size_t)b * a.ws_stride + WL.YV;
+  double* X = a.X + (size_t)b * a.P * n;
+  __shared__ double red[8];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  double dmax = 0.0, fin = 0.0;
+  for (int t = threadIdx.x; t < a.P * n; t += 256) {
+    const int j = t / n, c = t % n;
+    const double dv = YV[c * a.Pp + j];
+    if (!isfinite(dv)) fin = 1.0;
+    dmax = fmax(dmax, fabs(dv));
+  }
+  dmax = wave_max(dmax);
+  fin = wave_max(fin);
+  if (lane == 0) {
+    red[wave] = dmax;
+    red[4 + wave] = fin;
+  }
+  __syncthreads();
+  dmax = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+  fin = fmax(fmax(red[4], red[5]), fmax(red[6], red[7]));
+  __syncthreads();
+  if (fin != 0.0) {
+    if (threadIdx.x == 0) a.state[b] = MHE_STATUS_NONFINITE;
+    return;
+  }
+  double xmax = 0.0;
+  for (int t = threadIdx.x; t < a.P * n; t += 256) {
+    const int j = t / n, c = t % n;
+    const double xv = X[t] + YV[c * a.Pp + j];
+    X[t] = xv;
+    xmax = fmax(xmax, fabs(xv));
+  }
+  xmax = wave_max(xmax);
+  if (lane == 0) red[wave] = xmax;
+  __syncthreads();
+  xmax = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+  if (threadIdx.x == 0) {
+    a.iters[b] += 1;
+    if (dmax <= a.tol * (1.0 + xmax)) a.state[b] = MHE_STATUS_CONVERGED;
+  }
+}
+
+__global__ void k_big_init(int batch, int* state, int* iters) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < batch) {
+    state[b] = BIG_RUNNING;
+    iters[b] = 0;
+  }
+}
+
+__global__ void k_big_finish(int batch, int* state) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < batch && state[b] == BIG_RUNNING) state[b] = MHE_STATUS_MAX_ITER;
+}
+
+// ------------------------------------------------------------ constants
+__global__ void k_big_consts(int P, int M, int n, int p, const double* D, const double* cw, const double* Qw,
+                             const double* Rw, const double* Pw, char* cbuf) {
+  const BigConst CL = big_const_layout(P, M, n, p);
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
+  double* oD = (double*)(cbuf + CL.D);
+  double* oDt = (double*)(cbuf + CL.Dt);
+  double* oDCD = (double*)(cbuf + CL.DCD);
+  for (int e = gid; e < P * P; e += stride) {
+    const int k = e / P, j = e % P;
+    oD[e] = D[e];
+    oDt[j * P + k] = D[e];
+    // (D^T C D)[k][j] with C = diag(cw): element (row k, col j)
+    double s = 0.0;
+    for (int t = 0; t < P; ++t) s += D[t * P + k] * cw[t] * D[t * P + j];
+    oDCD[e] = s;
+  }
+  for (int e = gid; e < P; e += stride) ((double*)(cbuf + CL.cw))[e] = cw[e];
+  for (int e = gid; e < n * n; e += stride) {
+    ((double*)(cbuf + CL.Qw))[e] = Qw[e];
+    ((double*)(cbuf + CL.Pw))[e] = Pw ? Pw[e] : 0.0;
+  }
+  for (int e = gid; e < M * p * p; e += stride) ((double*)(cbuf + CL.Rw))[e] = Rw[e];
+}
+
+// epoch detection: row i starts an epoch unless its Phi row equals row i-1 bitwise
+__global__ void k_big_epoch_flags(int P, int M, int n, int p, const double* Phi, char* cbuf) {
+  const BigConst CL = big_const_layout(P, M, n, p);
+  int* flag = (int*)(cbuf + CL.flag);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < M; i += gridDim.x * blockDim.x) {
+    int f = (i == 0);
+    if (!f)
+      for (int j = 0; j < P; ++j)
+        if (__double_as_longlong(Phi[(size_t)i * P + j]) != __double_as_longlong(Phi[(size_t)(i - 1) * P + j])) {
+          f = 1;
+          break;
+        }
+    flag[i] = f;
+  }
+}
+
+__global__ void k_big_epoch_scan(int P, int M, int n, int p, char* cbuf) {
+  const BigConst CL = big_const_layout(P, M, n, p);
+  const int* flag = (const int*)(cbuf + CL.flag);
+  int* erow = (int*)(cbuf + CL.erow);
+  int E = 0;
+  for (int i = 0; i < M; ++i)
+    if (flag[i]) erow[E++] = i;
+  erow[E] = M;
+  *(int*)(cbuf + CL.ne) = E;
+}
+
+__global__ void k_big_epoch_rows(int P, int M, int n, int p, const double* Phi, char* cbuf) {
+  const BigConst CL = big_const_layout(P, M, n, p);
+  const int* erow = (const int*)(cbuf + CL.erow);
+  const int E = *(const int*)(cbuf + CL.ne);
+  double* PhiE = (double*)(cbuf + CL.PhiE);
+  double* PhiET = (double*)(cbuf + CL.PhiET);
+  const int Mr = M > 0 ? M : 1;
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < E * P; t += gridDim.x * blockDim.x) {
+    const int e = t / P, j = t % P;
+    const double v = Phi[(size_t)erow[e] * P + j];
+    PhiE[(size_t)e * P + j] = v;
+    PhiET[(size_t)j * Mr + e] = v;
+  }
+}

@@ -871,6 +871,8 @@ __device__ __forceinline__ void backward(const GnArgs& a, const SmemLayout& SL, 
   }
 }
 
+#include "mhe_big.h"
+
 template <class DYN, class MEAS, int SLOTS, int mode>
 __global__ __launch_bounds__(NTHREADS, 2) void k_gn(GnArgs a) {
   constexpr int n = DYN::n;
@@ -1132,6 +1134,15 @@ bool meas_info(int id, int n, int& p, int& q, bool& linear) {
   return false;
 }
 
+// Register-resident path iff the node-major padded system fits MAX_NT tiles.
+// MHE_FORCE_BIG=1 (tests only) routes every problem through the large-system
+// path so both paths can be compared on identical inputs.
+bool is_big(const mhe_dims* dm) {
+  const char* f = getenv("MHE_FORCE_BIG");
+  if (f && f[0] == '1') return true;
+  return ((dm->N + 1) * dm->n + 15) / 16 > MAX_NT;
+}
+
 int check_dims(const mhe_dims* dm, int* NT_out) {
   if (!dm) return MHE_ERR_NULL;
   int n, m, p, q;
@@ -1146,8 +1157,8 @@ int check_dims(const mhe_dims* dm, int* NT_out) {
         (dm->meas_model == MHE_MEAS_RANGE_3D && i < 3 && (dm->meas_idx[i] < 0 || dm->meas_idx[i] >= n)))
       return MHE_ERR_DIMS;
   const int P = dm->N + 1;
-  const int NT = (P * n + 15) / 16;
-  if (NT > MAX_NT) return MHE_ERR_UNSUPPORTED;
+  int NT = (P * n + 15) / 16;
+  if (is_big(dm)) NT = n * big_pp(P) / 16;  // large-system path (mhe_big.h), component-major tiles
   if (NT_out) *NT_out = NT;
   return MHE_OK;
 }
@@ -1178,6 +1189,16 @@ template <class MEAS>
 int launch_cc(const mhe_dims* dm, int NT, const double* D, const double* cw, const double* Phi,
               const double* Qw, const double* Rw, const double* Pw, char* cbuf, hipStream_t st) {
   const int P = dm->N + 1;
+  if (is_big(dm)) {
+    hipLaunchKernelGGL(k_big_consts, dim3(256), dim3(256), 0, st, P, dm->M, dm->n, dm->p, D, cw, Qw, Rw, Pw, cbuf);
+    if (dm->M > 0) {
+      hipLaunchKernelGGL(k_big_epoch_flags, dim3((dm->M + 255) / 256), dim3(256), 0, st, P, dm->M, dm->n, dm->p,
+                         Phi, cbuf);
+      hipLaunchKernelGGL(k_big_epoch_scan, dim3(1), dim3(1), 0, st, P, dm->M, dm->n, dm->p, cbuf);
+      hipLaunchKernelGGL(k_big_epoch_rows, dim3(256), dim3(256), 0, st, P, dm->M, dm->n, dm->p, Phi, cbuf);
+    }
+    return hipGetLastError() == hipSuccess ? MHE_OK : MHE_ERR_HIP;
+  }
   const int ntiles = NT * (NT + 1) / 2;
   hipLaunchKernelGGL(k_copy_consts, dim3(256), dim3(256), 0, st, P, dm->M, dm->n, dm->p, NT, D, cw, Phi, Qw,
                      Rw, Pw, cbuf);
@@ -1254,6 +1275,45 @@ struct LaunchGN {
   int run() { return launch_gn<DYN, MEAS>(dm, *a, batch, mode, st); }
 };
 
+// Large-system path: enqueue max_iter iterations of resid -> assemble -> chol -> update
+struct LaunchBig {
+  const mhe_dims* dm;
+  BigArgs* a;
+  int batch, max_iter;
+  const double* X0;
+  hipStream_t st;
+  template <class DYN, class MEAS>
+  int run() {
+    BigArgs& A = *a;
+    const int ntiles = A.NT * (A.NT + 1) / 2;
+    const size_t fixed = (size_t)(DTS + BIG_NW * 16 + 16 + 2) * sizeof(double);
+    const size_t lds_max = 160 * 1024 - 1024;
+    int cache = (int)((lds_max - fixed) / (256 * sizeof(double)));
+    if (cache > A.NT - 1) cache = A.NT - 1;
+    if (cache < 0) cache = 0;
+    A.cache_tiles = cache;
+    const int smem = (int)(fixed + (size_t)cache * 256 * sizeof(double));
+    if (hipFuncSetAttribute((const void*)k_big_chol, hipFuncAttributeMaxDynamicSharedMemorySize, smem) != hipSuccess)
+      return MHE_ERR_HIP;
+    if (hipMemcpyAsync(A.X, X0, sizeof(double) * batch * A.P * A.n, hipMemcpyDeviceToDevice, st) != hipSuccess)
+      return MHE_ERR_HIP;
+    hipLaunchKernelGGL(k_big_init, dim3((batch + 255) / 256), dim3(256), 0, st, batch, A.state, A.iters);
+    for (int it = 0; it < max_iter; ++it) {
+      hipLaunchKernelGGL((k_big_resid<DYN, MEAS>), dim3(batch), dim3(BIG_NTHREADS), 0, st, A, 0);
+      hipLaunchKernelGGL((k_big_assemble<DYN, MEAS>), dim3((ntiles + 3) / 4, batch), dim3(256), 0, st, A);
+      hipLaunchKernelGGL(k_big_chol, dim3(batch), dim3(BIG_NTHREADS), smem, st, A);
+      hipLaunchKernelGGL((k_big_update<DYN::n>), dim3(batch), dim3(256), 0, st, A);
+    }
+    hipLaunchKernelGGL((k_big_resid<DYN, MEAS>), dim3(batch), dim3(BIG_NTHREADS), 0, st, A, 1);
+    hipLaunchKernelGGL(k_big_finish, dim3((batch + 255) / 256), dim3(256), 0, st, batch, A.state);
+    return hipGetLastError() == hipSuccess ? MHE_OK : MHE_ERR_HIP;
+  }
+};
+
+size_t big_ws_doubles(const mhe_dims* dm, int NT) {
+  return big_ws_layout(dm->N + 1, dm->M, dm->n, NT).total;
+}
+
 }  // namespace
 
 #ifdef MHE_DIAG
@@ -1267,12 +1327,20 @@ const char* mhe_version(void) { return "libmhe 0.1 (gfx950, register-tiled fp64 
 int32_t mhe_padded_dim(const mhe_dims* dims) {
   int NT = 0;
   if (check_dims(dims, &NT) != MHE_OK) return -1;
-  return 16 * NT;
+  return 16 * NT;  // big path: n * Pp (component-major)
+}
+
+size_t mhe_workspace_bytes(const mhe_dims* dims, int32_t batch) {
+  int NT = 0;
+  if (check_dims(dims, &NT) != MHE_OK || batch < 0) return 0;
+  if (!is_big(dims)) return 0;
+  return sizeof(double) * big_ws_doubles(dims, NT) * (size_t)batch;
 }
 
 size_t mhe_const_bytes(const mhe_dims* dims) {
   int NT = 0;
   if (check_dims(dims, &NT) != MHE_OK) return 0;
+  if (is_big(dims)) return big_const_layout(dims->N + 1, dims->M, dims->n, dims->p).total;
   return const_layout(dims->N + 1, dims->M, dims->n, dims->p, NT).total;
 }
 
@@ -1292,6 +1360,14 @@ int mhe_gn_solve(const mhe_dims* dims, const void* const_buf, int32_t batch, con
                  const double* U, int64_t u_bstride, const double* Y, const double* PAR, int64_t par_bstride,
                  const double* x0, double* cost_out, int32_t* iters_out, int32_t* status_out, int32_t max_iter,
                  double tol, void* stream) {
+  return mhe_gn_solve_ws(dims, const_buf, batch, X0, X_out, U, u_bstride, Y, PAR, par_bstride, x0, cost_out,
+                         iters_out, status_out, max_iter, tol, nullptr, 0, stream);
+}
+
+int mhe_gn_solve_ws(const mhe_dims* dims, const void* const_buf, int32_t batch, const double* X0, double* X_out,
+                    const double* U, int64_t u_bstride, const double* Y, const double* PAR, int64_t par_bstride,
+                    const double* x0, double* cost_out, int32_t* iters_out, int32_t* status_out, int32_t max_iter,
+                    double tol, void* workspace, size_t workspace_bytes, void* stream) {
   int NT = 0;
   int rc = check_dims(dims, &NT);
   if (rc != MHE_OK) return rc;
@@ -1300,6 +1376,20 @@ int mhe_gn_solve(const mhe_dims* dims, const void* const_buf, int32_t batch, con
   if (!const_buf || !X0 || !X_out || !cost_out || !iters_out || !status_out || (dims->M > 0 && !Y) ||
       (dims->m > 0 && !U) || (dims->q > 0 && !PAR) || (dims->has_prior && !x0))
     return MHE_ERR_NULL;
+  if (is_big(dims)) {
+    if (!workspace || workspace_bytes < mhe_workspace_bytes(dims, batch)) return MHE_ERR_NULL;
+    BigArgs A = {};
+    A.cbuf = (const char*)const_buf;
+    A.P = dims->N + 1; A.M = dims->M; A.n = dims->n; A.Pp = big_pp(A.P); A.NTc = A.Pp / 16; A.NT = NT;
+    A.q = dims->q; A.has_prior = dims->has_prior;
+    for (int i = 0; i < 8; ++i) A.idx[i] = dims->meas_idx[i];
+    A.alpha = 2.0 / dims->T;
+    A.U = U; A.ustride = u_bstride; A.Y = Y; A.PAR = PAR; A.pstride = par_bstride; A.x0 = x0;
+    A.X = X_out; A.cost = cost_out; A.iters = iters_out; A.state = status_out; A.tol = tol;
+    A.ws = (double*)workspace; A.ws_stride = big_ws_doubles(dims, NT);
+    LaunchBig f{dims, &A, batch, max_iter, X0, (hipStream_t)stream};
+    return dispatch(dims, f);
+  }
   GnArgs a = make_args(dims, const_buf, NT);
   a.X0 = X0; a.Xout = X_out; a.U = U; a.ustride = u_bstride; a.Y = Y; a.PAR = PAR; a.pstride = par_bstride;
   a.x0 = x0; a.cost = cost_out; a.iters = iters_out; a.status = status_out; a.max_iter = max_iter; a.tol = tol;
@@ -1313,6 +1403,7 @@ int mhe_assemble(const mhe_dims* dims, const void* const_buf, int32_t batch, con
   int NT = 0;
   int rc = check_dims(dims, &NT);
   if (rc != MHE_OK) return rc;
+  if (is_big(dims)) return MHE_ERR_UNSUPPORTED;  // kernel-level parity APIs: register path only
   if (batch <= 0) return batch == 0 ? MHE_OK : MHE_ERR_DIMS;
   if (!const_buf || !X || !H || !g || !cost || (dims->M > 0 && !Y) || (dims->m > 0 && !U) ||
       (dims->q > 0 && !PAR) || (dims->has_prior && !x0))
@@ -1329,6 +1420,7 @@ int mhe_chol_solve(const mhe_dims* dims, const void* const_buf, int32_t batch, c
   int NT = 0;
   int rc = check_dims(dims, &NT);
   if (rc != MHE_OK) return rc;
+  if (is_big(dims)) return MHE_ERR_UNSUPPORTED;  // kernel-level parity APIs: register path only
   if (batch <= 0) return batch == 0 ? MHE_OK : MHE_ERR_DIMS;
   if (!const_buf || !H || !g || !delta || !status) return MHE_ERR_NULL;
   GnArgs a = make_args(dims, const_buf, NT);

@@ -41,6 +41,9 @@ SIGNATURES = {
     "mhe_build_constants": (ctypes.c_int, [_P, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "mhe_gn_solve": (ctypes.c_int, [_P, c_vp, c_i32, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp,
                                     c_vp, c_vp, c_vp, c_i32, c_dbl, c_vp]),
+    "mhe_workspace_bytes": (c_sz, [_P, c_i32]),
+    "mhe_gn_solve_ws": (ctypes.c_int, [_P, c_vp, c_i32, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp,
+                                       c_vp, c_vp, c_vp, c_i32, c_dbl, c_vp, c_sz, c_vp]),
     "mhe_assemble": (ctypes.c_int, [_P, c_vp, c_i32, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp,
                                     c_vp, c_vp, c_vp, c_vp]),
     "mhe_chol_solve": (ctypes.c_int, [_P, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),

@@ -8,6 +8,8 @@ C1  single_integrator: n=1, m=1, full_state, N=20, T=10, M=50, B=1
     (estimation_example.py:13,20,24,33 scales; u = sin t)
 C2  van_der_pol:       n=2, m=1 (u = 0), full_state, N=100, T=10, M=101, B=1024
     (van_der_pol.py:10,33 scales; R, Q from estimation_example.py:20,33)
+C3  gnss_stationary:   n=5, m=3, pseudorange, N=200, T=200, 201 epochs x 12 sats, B=4096
+    (large-system path: d = 1005)
 """
 import numpy as np
 from scipy.interpolate import interp1d
@@ -96,7 +98,6 @@ def make_c2(B=1024, seed=1, N=100):
                     X_init=_init_from_measurements(cpm, t, Y), X_true=xt, cpm=cpm)
 
 
-CONFIGS = {"C1": make_c1, "C2": make_c2}
 
 
 def make_gnss_small(B=4, seed=2, N=10, T=50.0, n_sat=8, epochs=51):
@@ -135,3 +136,15 @@ def make_gnss_small(B=4, seed=2, N=10, T=50.0, n_sat=8, epochs=51):
                     dyn="gnss_pos_and_bias", meas="pseudorange", meas_static={"idx": [0, 1, 2, 3]},
                     t_meas=t_meas, Y=Y, U=np.zeros((1, N + 1, 3)), PAR=PAR, Qw=np.linalg.inv(Q),
                     Rw=np.full((M, 1, 1), 1.0 / r_pr), Pw=None, x0=None, X_init=X_init, X_true=xt, cpm=cpm)
+
+
+def make_c3(B=4096, seed=2, N=200):
+    """C3 gnss_stationary shape: gnss_pos_and_bias (n=5, m=3, u=0) +
+    pseudorange, N=200, T=200 s, 201 epochs x 12 satellite slots (M=2412), d=1005.
+    Synthetic satellite geometry (the reference's .mat ephemerides stay off the box)."""
+    w = make_gnss_small(B=B, seed=seed, N=N, T=200.0, n_sat=12, epochs=201)
+    w.name = "C3_gnss_stationary"
+    return w
+
+
+CONFIGS = {"C1": make_c1, "C2": make_c2, "C3": make_c3}

@@ -92,6 +92,7 @@ class BatchSolver:
         self._src = {k: _dev(v, dev) for k, v in self._host.items() if v is not None}
         self.cbuf = torch.empty(nbytes, dtype=torch.uint8, device=dev)
         Pw_t = self._src.get("Pw")
+        self._ws = None
         rc = self.lib.mhe_build_constants(
             self.dims, _ptr(self._src["D"]), _ptr(self._src["cw"]), _ptr(self._src["Phi"]),
             _ptr(self._src["Qw"]), _ptr(self._src["Rw"]), _ptr(Pw_t), _ptr(self.cbuf), _stream(None))
@@ -128,6 +129,27 @@ class BatchSolver:
             x0_t = _dev(x0, dev, (B, self.n))
         return X, B, U_t, ustr, Y_t, PAR_t, pstr, x0_t
 
+    @property
+    def large_system(self):
+        """True when the problem exceeds the register-resident kernel (C3-C5):
+        mhe_gn_solve_ws then needs a device workspace (allocated here, cached)."""
+        return self.lib.mhe_workspace_bytes(self.dims, 1) > 0
+
+    def _workspace(self, B):
+        nb = self.lib.mhe_workspace_bytes(self.dims, B)
+        if nb == 0:
+            return None, 0
+        if self._ws is None or self._ws.numel() < nb:
+            self._ws = torch.empty(nb, dtype=torch.uint8, device=self.device)
+        return self._ws, nb
+
+    def _gn(self, B, X, Xo, U_t, ustr, Y_t, PAR_t, pstr, x0_t, cost, iters, status, max_iter, tol, stream):
+        ws, nb = self._workspace(B)
+        rc = self.lib.mhe_gn_solve_ws(self.dims, _ptr(self.cbuf), B, _ptr(X), _ptr(Xo), _ptr(U_t), ustr, _ptr(Y_t),
+                                      _ptr(PAR_t), pstr, _ptr(x0_t), _ptr(cost), _ptr(iters), _ptr(status),
+                                      int(max_iter), float(tol), _ptr(ws), nb, _stream(stream))
+        _lib.check(rc, "mhe_gn_solve_ws")
+
     # ------------------------------------------------------------------ calls
     def solve(self, X0, U, Y, PAR=None, x0=None, max_iter=20, tol=1e-10, stream=None, out=None):
         """Gauss-Newton to convergence. Returns (X, cost, iters, status) device tensors."""
@@ -139,10 +161,7 @@ class BatchSolver:
             status = torch.empty(B, dtype=torch.int32, device=self.device)
         else:
             Xo, cost, iters, status = out
-        rc = self.lib.mhe_gn_solve(self.dims, _ptr(self.cbuf), B, _ptr(X), _ptr(Xo), _ptr(U_t), ustr, _ptr(Y_t),
-                                   _ptr(PAR_t), pstr, _ptr(x0_t), _ptr(cost), _ptr(iters), _ptr(status),
-                                   int(max_iter), float(tol), _stream(stream))
-        _lib.check(rc, "mhe_gn_solve")
+        self._gn(B, X, Xo, U_t, ustr, Y_t, PAR_t, pstr, x0_t, cost, iters, status, max_iter, tol, stream)
         return Xo, cost, iters, status
 
     def prepare(self, X0, U, Y, PAR=None, x0=None):
@@ -152,10 +171,7 @@ class BatchSolver:
     def solve_staged(self, staged, outs, max_iter, tol, stream=None):
         X, B, U_t, ustr, Y_t, PAR_t, pstr, x0_t = staged
         Xo, cost, iters, status = outs
-        rc = self.lib.mhe_gn_solve(self.dims, _ptr(self.cbuf), B, _ptr(X), _ptr(Xo), _ptr(U_t), ustr, _ptr(Y_t),
-                                   _ptr(PAR_t), pstr, _ptr(x0_t), _ptr(cost), _ptr(iters), _ptr(status),
-                                   int(max_iter), float(tol), _stream(stream))
-        _lib.check(rc, "mhe_gn_solve")
+        self._gn(B, X, Xo, U_t, ustr, Y_t, PAR_t, pstr, x0_t, cost, iters, status, max_iter, tol, stream)
 
     def assemble(self, X, U, Y, PAR=None, x0=None, stream=None):
         """GN normal equations at X: H (B,dp,dp), g (B,dp), cost (B)."""

@@ -35,5 +35,7 @@ def test_host_side_entry_points_without_gpu():
     assert lib.mhe_padded_dim(d) == -1
     d.n, d.dyn_model = 2, 99
     assert lib.mhe_const_bytes(d) == 0
-    d.dyn_model, d.N = 5, 500  # beyond the register-resident limit of this build
-    assert lib.mhe_padded_dim(d) == -1
+    assert lib.mhe_workspace_bytes(d, 1024) == 0  # register-resident path needs no workspace
+    d.dyn_model, d.N = 5, 500  # beyond the register-resident limit: large-system path
+    assert lib.mhe_padded_dim(d) == 2 * 512  # component-major, P padded to 16 per component
+    assert lib.mhe_workspace_bytes(d, 2) > 2 * 8 * (64 * 65 // 2) * 256

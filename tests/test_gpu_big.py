@@ -1,0 +1,118 @@
+"""Large-system GN path (csrc/mhe_big.h: workspace, HBM-resident tiles) vs the
+register-resident kernel and the CPU oracle.
+
+Tolerances as tests/test_gpu_parity.py: iterates <= 1e-9 kappa (1 + max|X|) after
+the same number of iterations, converged optimum <= 1e-8 kappa (1 + max|X|),
+kappa = max|y| / max|y - h(x)| (pseudorange cancellation); iteration counts and
+statuses exact.  MHE_FORCE_BIG=1 (debug knob) routes C2 through the large-system
+path, so the two device paths are compared on identical inputs.
+"""
+import os
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+from mhe import configs, solver  # noqa: E402
+from oracle import gn  # noqa: E402
+
+
+def _problem(w):
+    return gn.Problem(w.N, w.T, w.n, w.m, w.dyn, w.meas, w.cpm.D, (w.T / 2) * w.cpm.w,
+                      w.cpm.lagrange_matrix(w.t_meas), w.Qw, w.Rw, Pw=w.Pw, meas_static=w.meas_static)
+
+
+def _U(w):
+    return np.broadcast_to(w.U, (w.B,) + w.U.shape[1:])
+
+
+def _PAR(w):
+    return None if w.PAR is None else np.broadcast_to(w.PAR, (w.B,) + w.PAR.shape[1:])
+
+
+def _kappa(w, pb, X):
+    _, _, e, _ = gn.residuals(pb, X, _U(w), w.Y, _PAR(w))
+    return max(1.0, np.abs(w.Y).max() / np.abs(e).max())
+
+
+def _np(ts):
+    return [t.cpu().numpy() for t in ts]
+
+
+def _forced_big(w):
+    os.environ["MHE_FORCE_BIG"] = "1"
+    try:
+        s = solver.from_workload(w)
+        assert s.large_system
+        return s
+    finally:
+        os.environ.pop("MHE_FORCE_BIG", None)
+
+
+def _solve_forced(s, w, **kw):
+    os.environ["MHE_FORCE_BIG"] = "1"
+    try:
+        out = _np(s.solve(w.X_init, w.U, w.Y, w.PAR, **kw))
+        torch.cuda.synchronize()
+        return out
+    finally:
+        os.environ.pop("MHE_FORCE_BIG", None)
+
+
+def test_forced_big_path_matches_register_path_c2():
+    w = configs.make_c2(B=8, N=100)
+    sr = solver.from_workload(w)
+    assert not sr.large_system
+    Xr, cr, ir, str_ = _np(sr.solve(w.X_init, w.U, w.Y, max_iter=4, tol=0.0))
+    sb = _forced_big(w)
+    Xb, cb, ib, stb = _solve_forced(sb, w, max_iter=4, tol=0.0)
+    assert ib.tolist() == ir.tolist() == [4] * w.B and stb.tolist() == str_.tolist()
+    assert np.abs(Xb - Xr).max() <= 1e-9 * (1 + np.abs(Xr).max())
+    assert np.allclose(cb, cr, rtol=1e-9)
+    # converged: same optimum, same statuses
+    Xr, cr, ir, str_ = _np(sr.solve(w.X_init, w.U, w.Y, max_iter=50, tol=1e-9))
+    Xb, cb, ib, stb = _solve_forced(sb, w, max_iter=50, tol=1e-9)
+    assert stb.tolist() == str_.tolist() == [0] * w.B
+    assert np.all(np.abs(ib - ir) <= 1)
+    assert np.abs(Xb - Xr).max() <= 1e-8 * (1 + np.abs(Xr).max())
+
+
+def test_big_vdp_n150_matches_oracle():
+    w = configs.make_c2(B=3, N=150)  # d = 302 > 208: large-system path by size
+    s = solver.from_workload(w)
+    assert s.large_system
+    X, cost, iters, status = _np(s.solve(w.X_init, w.U, w.Y, max_iter=3, tol=0.0))
+    pb = _problem(w)
+    Xr, cr, ir, sr = gn.gauss_newton(pb, w.X_init, _U(w), w.Y, max_iter=3, tol=0.0)
+    assert iters.tolist() == ir.tolist() and status.tolist() == sr.tolist()
+    assert np.abs(X - Xr).max() <= 1e-9 * (1 + np.abs(Xr).max())
+    assert np.allclose(cost, cr, rtol=1e-9)
+
+
+@pytest.mark.parametrize("N", [60, 200])
+def test_big_gnss_matches_oracle(N):
+    """N=200 is the C3 shape (d = 1005, 201 epochs x 12 pseudoranges)."""
+    w = configs.make_gnss_small(B=2, N=N, T=float(N), n_sat=12, epochs=N + 1)
+    s = solver.from_workload(w)
+    assert s.large_system
+    pb = _problem(w)
+    X, cost, iters, status = _np(s.solve(w.X_init, w.U, w.Y, w.PAR, max_iter=3, tol=0.0))
+    Xr, cr, ir, sr = gn.gauss_newton(pb, w.X_init, _U(w), w.Y, _PAR(w), max_iter=3, tol=0.0)
+    k = _kappa(w, pb, Xr)
+    assert iters.tolist() == ir.tolist() and status.tolist() == sr.tolist()
+    assert np.abs(X - Xr).max() <= 1e-9 * k * (1 + np.abs(Xr).max())
+    assert np.allclose(cost, cr, rtol=1e-9 * k)
+
+
+def test_big_max_iter_zero_and_empty_batch():
+    w = configs.make_c2(B=2, N=150)
+    s = solver.from_workload(w)
+    X, cost, iters, status = _np(s.solve(w.X_init, w.U, w.Y, max_iter=0))
+    assert np.array_equal(X, w.X_init) and iters.tolist() == [0, 0] and status.tolist() == [1, 1]
+    _, _, _, cr = gn.residuals(_problem(w), w.X_init, _U(w), w.Y)
+    assert np.allclose(cost, cr, rtol=1e-12)
+    X, cost, iters, status = s.solve(np.zeros((0, w.P, w.n)), w.U, np.zeros((0, w.M, w.p)), max_iter=3)
+    assert X.shape == (0, w.P, w.n)
