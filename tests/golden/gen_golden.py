@@ -256,11 +256,75 @@ def gen_ekf(ref):
                         mu=np.stack(mus), S=np.stack(Ss), dt=np.array(1.0))
 
 
+def gen_gnss_io(ref):
+    """GNSS on-disk format (utils/data.py:9-75) and geodesy (utils/utils.py:4-110).
+
+    Inputs: a reduced copy of the gnss_stationary log -- the SVID row plus the first
+    60 epochs of ``svPoss`` (T+1,12,5) and ``pseudoranges`` (T+1,12) -- written with
+    scipy.io.savemat, and a 3-D ``pseudoranges`` variant (T+1,12,6: range, rate,
+    velocity, time) built from it with seeded rates/velocities.  Expected outputs:
+    the reference ``load_gnss_logs`` run on those files (ragged per-epoch lists
+    padded to 12 slots + counts) and the reference geodesy on seeded points."""
+    from scipy.io import loadmat, savemat
+    src = f"{REF}/data/gnss_stationary/gnss_log_2020_02_05_09_14_15"
+    sv = loadmat(src + "satposecef.mat")["svPoss"][:61].copy()
+    pr = loadmat(src + "ranges.mat")["pseudoranges"][:61].copy()
+    small = os.path.join(OUT, "gnss_small_")
+    savemat(small + "satposecef.mat", {"svPoss": sv})
+    savemat(small + "ranges.mat", {"pseudoranges": pr})
+    rng = np.random.default_rng(11)
+    pr3 = np.zeros(pr.shape + (6,))
+    pr3[:, :, 0] = pr
+    pr3[1:, :, 1] = rng.normal(size=(60, 12)) * 100.0
+    pr3[1:, :, 2:5] = rng.normal(size=(60, 12, 3)) * 3e3
+    pr3[1:, :, 5] = 1000.0 + np.arange(60)[:, None] + rng.uniform(0, 0.01, size=(60, 12))
+    pr3[0, :, 0] = pr[0]
+    small3 = os.path.join(OUT, "gnss_small3_")
+    savemat(small3 + "satposecef.mat", {"svPoss": sv})
+    savemat(small3 + "ranges.mat", {"pseudoranges": pr3})
+    out = {}
+    for tag, prefix in (("d2", small), ("d3", small3)):
+        d = ref.data.load_gnss_logs(prefix)
+        T = len(d["pr"])
+        cnt = np.array([len(x) for x in d["pr"]], dtype=np.int32)
+        sp = np.zeros((T, 12, 3))
+        pv = np.zeros((T, 12))
+        for k in range(T):
+            sp[k, :cnt[k]] = d["sat_pos"][k]
+            pv[k, :cnt[k]] = d["pr"][k]
+        out[f"{tag}_t"] = np.asarray(list(d["t"]), dtype=np.float64)
+        out[f"{tag}_sats"] = np.asarray(d["sats"], dtype=np.float64)
+        out[f"{tag}_count"], out[f"{tag}_sat_pos"], out[f"{tag}_pr"] = cnt, sp, pv
+        if "sat_vel" in d:
+            sv3 = np.zeros((T, 12, 3))
+            rr = np.zeros((T, 12))
+            for k in range(T):
+                sv3[k, :cnt[k]] = d["sat_vel"][k]
+                rr[k, :cnt[k]] = d["pr_rate"][k]
+            out[f"{tag}_sat_vel"], out[f"{tag}_pr_rate"] = sv3, rr
+    # geodesy on seeded points around the reference site (and far away)
+    lla = np.stack([rng.uniform(-80, 80, 32), rng.uniform(-180, 180, 32), rng.uniform(-100, 9000, 32)], axis=1)
+    lla[0] = [37.4276, -122.1670, 0.0]
+    ecef = np.stack([ref.gutils.lla2ecef(p) for p in lla])
+    out["geo_lla_in"], out["geo_ecef"] = lla, ecef
+    out["geo_lla_back"] = np.stack([ref.gutils.ecef2lla(p) for p in ecef])
+    pts = ecef[0] + rng.normal(size=(32, 3)) * 2e4
+    out["geo_pts"] = pts
+    out["geo_enu"] = np.stack([ref.gutils.ecef2enu(p, ecef[0]) for p in pts])
+    out["geo_enu_rot"] = np.stack([ref.gutils.ecef2enu(p, ecef[0], rotation_only=True) for p in pts])
+    out["geo_enu2ecef"] = np.stack([ref.gutils.enu2ecef(e, ecef[0]) for e in out["geo_enu"]])
+    tt = np.round(rng.uniform(0, 100, 200), 1)
+    out["ti_t"] = tt
+    out["ti_idx"] = ref.gutils.get_time_indices(tt, 20.0, 35.5).astype(np.int64)
+    np.savez_compressed(os.path.join(OUT, "gnss_io.npz"), **out)
+
+
 def main():
     ref = load_reference()
     gen_collocation(ref)
     gen_plugins(ref)
     gen_ekf(ref)
+    gen_gnss_io(ref)
     print("golden fixtures written to", OUT)
 
 

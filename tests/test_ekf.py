@@ -162,3 +162,34 @@ def test_ekf_bias_row_variant(golden):
     rmu, rS = _oracle_batch(fx, mu0, S0, U, Z, nz, sat13, meas=oekf.multi_pseudorange_and_bias, extra=1)
     emu, eS = _close(mh.cpu().numpy(), Sh.cpu().numpy(), rmu, rS)
     assert emu <= MU_TOL and eS <= S_TOL, (emu, eS)
+
+
+@pytest.mark.gpu
+def test_ekf_end_to_end_from_log_files():
+    """On-disk log (reduced gnss_stationary .mat, utils.data) -> fixed-slot device
+    layout (pack_epochs, ENU at the reference site) -> batched EKF, vs the oracle EKF
+    fed the reference loader's per-epoch arrays."""
+    import os
+    from utils import data as gdata, utils as gutils
+    G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    d = gdata.load_gnss_logs(os.path.join(G, "gnss_small_"))
+    p_ref = gutils.lla2ecef(np.array([37.4276, -122.1670, 0.0]))
+    pk = gdata.pack_epochs(d, p_ref, slots=12)
+    T = pk["pr"].shape[0]
+    B = 4
+    mu0 = np.tile(np.array([10.0, -5.0, 3.0, 1.0, 0.5]), (B, 1)) + np.arange(B)[:, None]
+    S0 = np.tile(np.eye(5), (B, 1, 1))
+    Q = np.diag([1e-4, 1e-4, 1e-4, 0.1, 1e-3])
+    R = np.tile(np.eye(12) * 100.0, (T, 1, 1))
+    mh, Sh, _, _, st = ekf.run_batch(gnss.gnss_pos_and_bias, gnss.multi_pseudorange, mu0, S0, np.zeros((B, T, 3)),
+                                     np.tile(pk["pr"], (B, 1, 1)), np.tile(pk["count"], (B, 1)), Q, R, 1.0,
+                                     np.tile(pk["sat_pos"], (B, 1, 1, 1)))
+    assert int(st.abs().sum().item()) == 0
+    for b in range(B):
+        f = oekf.EKF(oekf.gnss_pos_and_bias, oekf.multi_pseudorange, mu0[b], S0[b])
+        for k in range(T):
+            sat = gutils.ecef2enu(d["sat_pos"][k], p_ref)
+            f.update(np.zeros(3), d["pr"][k], Q, np.diag(100.0 * np.ones(len(d["pr"][k]))), {"dt": 1.0}, None,
+                     {"sat_pos": sat})
+            emu, eS = _close(mh[b, k].cpu().numpy()[None], Sh[b, k].cpu().numpy()[None], f.mu[None], f.S[None])
+            assert emu <= MU_TOL and eS <= S_TOL, (b, k, emu, eS)
