@@ -84,7 +84,20 @@ typedef struct mhe_dims {
   int32_t has_prior;    /* 1: addInitialCost term present                    */
   int32_t meas_idx[8];  /* static index params (params["idx"]), model-defined */
   double T;             /* window length; node times tau2t(tau)              */
+  int32_t dyn_cost;     /* MHE_COST_L2 (weighted_l2_norm) or MHE_COST_HUBER  */
+  int32_t n_bounds;     /* addVarBounds: number of bounded state components  */
+  double huber_delta;   /* pseudo_huber_loss params["delta"]                 */
+  int32_t bound_idx[8]; /* bounded component indices (< n)                   */
+  double bound_lb[8];   /* lower / upper bounds (+-inf allowed), every node  */
+  double bound_ub[8];
 } mhe_dims;
+
+/* Dynamics cost (addDynamicsCost, nlp/nlp.py:242-245): */
+#define MHE_COST_L2 0     /* cost_functions.weighted_l2_norm  (cost_functions.py:20-22) */
+#define MHE_COST_HUBER 1  /* cost_functions.pseudo_huber_loss (cost_functions.py:25-31): IRLS
+                             weights q_a / sqrt(1 + W_a^2 / delta^2), only diag(Qw) enters */
+/* Bounds (addVarBounds, nlp/nlp.py:314-317) are enforced by projecting every GN
+ * step onto the box (projected Gauss-Newton). */
 
 /* Size in bytes of the device constants buffer for `dims` (0 on bad dims). */
 size_t mhe_const_bytes(const mhe_dims* dims);

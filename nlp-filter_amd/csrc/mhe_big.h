@@ -96,6 +96,9 @@ struct BigArgs {
   double* ws;      // workspace base
   size_t ws_stride;  // doubles per trajectory
   int cache_tiles;   // block-column tiles cached in LDS by k_big_chol
+  int n_bounds;      // projected GN (addVarBounds)
+  int bidx[8];
+  double blb[8], bub[8];
 };
 
 __device__ __forceinline__ int big_tile_index(int I, int J, int NT) { return J * NT - J * (J - 1) / 2 + (I - J); }
@@ -460,7 +463,13 @@ __global__ __launch_bounds__(256) void k_big_update(BigArgs a) {
     const int j = t / n, c = t % n;
     const double dv = YV[c * a.Pp + j];
     if (!isfinite(dv)) fin = 1.0;
-    dmax = fmax(dmax, fabs(dv));
+    double step = dv;
+    for (int i = 0; i < a.n_bounds; ++i)
+      if (a.bidx[i] == c) {
+        const double xv = X[t] + dv, xc = fmin(fmax(xv, a.blb[i]), a.bub[i]);
+        if (xc != xv) step = xc - X[t];
+      }
+    dmax = fmax(dmax, fabs(step));
   }
   dmax = wave_max(dmax);
   fin = wave_max(fin);
@@ -479,7 +488,9 @@ __global__ __launch_bounds__(256) void k_big_update(BigArgs a) {
   double xmax = 0.0;
   for (int t = threadIdx.x; t < a.P * n; t += 256) {
     const int j = t / n, c = t % n;
-    const double xv = X[t] + YV[c * a.Pp + j];
+    double xv = X[t] + YV[c * a.Pp + j];
+    for (int i = 0; i < a.n_bounds; ++i)
+      if (a.bidx[i] == c) xv = fmin(fmax(xv, a.blb[i]), a.bub[i]);
     X[t] = xv;
     xmax = fmax(xmax, fabs(xv));
   }

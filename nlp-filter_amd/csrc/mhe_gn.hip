@@ -67,7 +67,7 @@ __host__ __device__ inline ConstLayout const_layout(int P, int M, int n, int p, 
 }
 
 struct SmemLayout {  // offsets in doubles
-  int Xs, Vs, FtV, Es, FtE, GE, G, BV, YV, PB, DT, RED, total;
+  int Xs, Vs, FtV, Es, FtE, GE, G, LAM, BV, YV, PB, DT, RED, total;
 };
 
 __host__ __device__ inline int rnd2(int x) { return (x + 1) & ~1; }  // keep 16-B alignment
@@ -86,6 +86,7 @@ __host__ __device__ inline SmemLayout smem_layout(int P, int M, int n, int NT, b
   S.FtE = o;  o += rnd2(P * n * n);
   S.GE = o;   o += rnd2(M * n);
   S.G = o;    o += nonlinear ? rnd2(M * n * n) : 0;
+  S.LAM = o;  o += rnd2(P * n);         // Huber IRLS weights c_k lambda_ka (MHE_COST_HUBER)
   S.BV = o;   o += dp;                  // right-hand side b = -g, updated block by block
   S.YV = o;   o += dp;                  // y = U^-T b, then delta = U^-1 y in place
   S.PB = o;   o += (NT - 1) * 256;      // block row k of U (tiles U_kb, b > k), register order
@@ -119,6 +120,10 @@ struct GnArgs {
   const double* gin;
   double* dout;
   unsigned long long* dbg;  // MHE_DIAG builds only: per-phase cycle sums
+  double huber_delta;       // MHE_COST_HUBER only
+  int n_bounds;             // projected GN: components bidx[i] clipped to [blb, bub]
+  int bidx[8];
+  double blb[8], bub[8];
 };
 
 #ifdef MHE_DIAG
@@ -257,7 +262,7 @@ __device__ __forceinline__ void dot_rows_half(const double* __restrict__ Mt, int
 // Per-node dynamics quantities (nlp/nlp.py:225-245):
 //   W_k = a * sum_j D_kj X_j - f(X_k, U_k);  V_k = c_k Qw W_k;  E_k = c_k Qw F_k;
 //   FtE_k = F_k^T E_k;  FtV_k = F_k^T V_k;   cost += c_k W_k^T Qw W_k
-template <class DYN>
+template <class DYN, bool HUBER = false>
 __device__ __forceinline__ double node_phase(const GnArgs& a, const ConstLayout& CL, const SmemLayout& SL, double* sm, int b) {
   constexpr int n = DYN::n, m = DYN::m;
   const double* Dt = (const double*)(a.cbuf + CL.Dt);
@@ -286,24 +291,41 @@ __device__ __forceinline__ double node_phase(const GnArgs& a, const ConstLayout&
 #pragma unroll
     for (int c = 0; c < n; ++c) W[c] = a.alpha * dx[c] - f[c];
     const double ck = cw[k];
-#pragma unroll
-    for (int r = 0; r < n; ++r) {
-      double s = 0.0;
-#pragma unroll
-      for (int c = 0; c < n; ++c) s += Qw[r * n + c] * W[c];
-      V[r] = ck * s;
-      cost += W[r] * V[r];
-    }
     double E[n * n];
+    if constexpr (HUBER) {
+      // pseudo_huber_loss (cost_functions.py:25-31), IRLS: lambda = q / sqrt(1 + W^2/delta^2),
+      // V = c lambda W (= c rho'/2), E = c diag(lambda) F
+      const double dl = a.huber_delta;
 #pragma unroll
-    for (int r = 0; r < n; ++r)
+      for (int r = 0; r < n; ++r) {
+        const double q = Qw[r * n + r];
+        const double sr = sqrt(1.0 + W[r] * W[r] / (dl * dl));
+        const double lam = ck * (q / sr);
+        V[r] = lam * W[r];
+        cost += ck * (2.0 * q * dl * dl * (sr - 1.0));
+        sm[SL.LAM + k * n + r] = lam;
 #pragma unroll
-      for (int c = 0; c < n; ++c) {
+        for (int c = 0; c < n; ++c) E[r * n + c] = lam * F[r * n + c];
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < n; ++r) {
         double s = 0.0;
 #pragma unroll
-        for (int t = 0; t < n; ++t) s += Qw[r * n + t] * F[t * n + c];
-        E[r * n + c] = ck * s;
+        for (int c = 0; c < n; ++c) s += Qw[r * n + c] * W[c];
+        V[r] = ck * s;
+        cost += W[r] * V[r];
       }
+#pragma unroll
+      for (int r = 0; r < n; ++r)
+#pragma unroll
+        for (int c = 0; c < n; ++c) {
+          double s = 0.0;
+#pragma unroll
+          for (int t = 0; t < n; ++t) s += Qw[r * n + t] * F[t * n + c];
+          E[r * n + c] = ck * s;
+        }
+    }
     double* Vs = sm + SL.Vs + k * n;
     double* FtV = sm + SL.FtV + k * n;
     double* Es = sm + SL.Es + k * n * n;
@@ -474,14 +496,24 @@ __device__ __forceinline__ double grad_phase(const GnArgs& a, const ConstLayout&
 
 // One 16x16 tile element of H at (row, col) in the MFMA C-layout position of
 // this lane (see build_tiles).
-template <class DYN, class MEAS>
+template <class DYN, class MEAS, bool HUBER = false>
 __device__ __forceinline__ double h_element(const GnArgs& a, const double* Phi, const double* Es,
                                             const double* FtE, const double* G, double v, double da,
-                                            double db, int row, int col) {
+                                            double db, int row, int col, const double* D = nullptr,
+                                            const double* LAM = nullptr) {
   constexpr int n = DYN::n;
   if (row < a.d && col < a.d) {
     const int j = row / n, aa = row - j * n;
     const int l = col / n, bb = col - l * n;
+    if constexpr (HUBER) {
+      // a^2 sum_k D_kj c_k lambda_ka D_kl (a == b): the dynamics "constant" part with
+      // iteration-dependent IRLS weights (excluded from Cc for MHE_COST_HUBER)
+      if (aa == bb) {
+        double s = 0.0;
+        for (int k = 0; k < a.P; ++k) s += D[k * a.P + j] * LAM[k * n + aa] * D[k * a.P + l];
+        v += a.alpha * a.alpha * s;
+      }
+    }
     v -= da * Es[(l * n + aa) * n + bb] + db * Es[(j * n + bb) * n + aa];
     if (j == l) v += FtE[(j * n + aa) * n + bb];
     if (!MEAS::LINEAR) {
@@ -504,9 +536,11 @@ __device__ __forceinline__ double h_element(const GnArgs& a, const double* Phi, 
 // Cc, DA = a D_lj and DB = a D_jl are stored per tile element in the MFMA
 // C-layout, so each is one coalesced 512-B load per register.  Off-diagonal
 // tiles go to the accumulator slots, diagonal tiles (owner wave J % NW) to LDS.
-template <class DYN, class MEAS, int SLOTS>
+template <class DYN, class MEAS, int SLOTS, bool HUBER = false>
 __device__ __forceinline__ void build_tiles(const GnArgs& a, const ConstLayout& CL, const SmemLayout& SL, double* sm,
                                             d4 (&acc)[SLOTS], int wave, int lane, int stab) {
+  const double* Dm = (const double*)(a.cbuf + CL.D);
+  const double* LAM = sm + SL.LAM;
   const double* Cc = (const double*)(a.cbuf + CL.Cc);
   const double* DA = (const double*)(a.cbuf + CL.DA);
   const double* DB = (const double*)(a.cbuf + CL.DB);
@@ -529,8 +563,8 @@ __device__ __forceinline__ void build_tiles(const GnArgs& a, const ConstLayout& 
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = 16 * J + (lane >> 4) + 4 * r;
-        acc[s][r] = -h_element<DYN, MEAS>(a, Phi, Es, FtE, G, Cc[off + 64 * r], DA[off + 64 * r],
-                                          DB[off + 64 * r], row, col);
+        acc[s][r] = -h_element<DYN, MEAS, HUBER>(a, Phi, Es, FtE, G, Cc[off + 64 * r], DA[off + 64 * r],
+                                                 DB[off + 64 * r], row, col, Dm, LAM);
       }
     }
     // bound the scheduler's load hoisting to two slots (register pressure)
@@ -543,8 +577,9 @@ __device__ __forceinline__ void build_tiles(const GnArgs& a, const ConstLayout& 
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int tr = (lane >> 4) + 4 * r;
-      DT[J * DTS + tr * 16 + (lane & 15)] = -h_element<DYN, MEAS>(a, Phi, Es, FtE, G, Cc[off + 64 * r], DA[off + 64 * r],
-                                                                  DB[off + 64 * r], 16 * J + tr, col);
+      DT[J * DTS + tr * 16 + (lane & 15)] = -h_element<DYN, MEAS, HUBER>(a, Phi, Es, FtE, G, Cc[off + 64 * r],
+                                                                         DA[off + 64 * r], DB[off + 64 * r],
+                                                                         16 * J + tr, col, Dm, LAM);
     }
   }
 }
@@ -873,7 +908,7 @@ __device__ __forceinline__ void backward(const GnArgs& a, const SmemLayout& SL, 
 
 #include "mhe_big.h"
 
-template <class DYN, class MEAS, int SLOTS, int mode>
+template <class DYN, class MEAS, int SLOTS, int mode, bool HUBER = false>
 __global__ __launch_bounds__(NTHREADS, 2) void k_gn(GnArgs a) {
   constexpr int n = DYN::n;
   extern __shared__ __attribute__((aligned(16))) double sm[];
@@ -914,7 +949,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void k_gn(GnArgs a) {
   DIAG_DECL
   for (;;) {
     DIAG_MARK(7);
-    double c1 = node_phase<DYN>(a, CL, SL, sm, b);
+    double c1 = node_phase<DYN, HUBER>(a, CL, SL, sm, b);
     c1 += meas_phase<DYN, MEAS>(a, CL, SL, sm, b);
     __syncthreads();
     DIAG_MARK(0);
@@ -923,7 +958,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void k_gn(GnArgs a) {
     if constexpr (mode == MODE_ASSEMBLE) {
       double c2 = 0.0;
       block_reduce2(RED, c1, c2, false);
-      build_tiles<DYN, MEAS, SLOTS>(a, CL, SL, sm, acc, wave, lane, stab);
+      build_tiles<DYN, MEAS, SLOTS, HUBER>(a, CL, SL, sm, acc, wave, lane, stab);
       const int dp = 16 * a.NT;
       double* Hb = a.Hout + (size_t)b * dp * dp;
 #pragma unroll
@@ -949,7 +984,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void k_gn(GnArgs a) {
       return;
     }
     if (it >= a.max_iter) break;
-    build_tiles<DYN, MEAS, SLOTS>(a, CL, SL, sm, acc, wave, lane, stab);
+    build_tiles<DYN, MEAS, SLOTS, HUBER>(a, CL, SL, sm, acc, wave, lane, stab);
     __syncthreads();
     DIAG_MARK(2);
     const bool ok = factor_forward<SLOTS>(a, SL, sm, acc, wave, lane, stab, DIAG_FARGS);
@@ -960,32 +995,40 @@ __global__ __launch_bounds__(NTHREADS, 2) void k_gn(GnArgs a) {
     }
     backward<SLOTS>(a, SL, sm, acc, wave, lane, stab);
     DIAG_MARK(4);
+    // X += delta, projected onto the bounds (addVarBounds); the convergence test uses
+    // |delta| for unclipped components and the actual move for clipped ones.  A
+    // non-finite delta is flagged as an infinite step (NONFINITE, X untouched).
     double dmax = 0.0, xmax = 0.0;
-    bool finite = true;
     const int tid_u = opaque_tid();
     for (int t = tid_u; t < a.d; t += NTHREADS) {
       const double dv = DV[t];
-      finite = finite && isfinite(dv);
-      dmax = fmax(dmax, fabs(dv));
+      double xv = Xs[t] + dv, step = dv;
+      for (int i = 0; i < a.n_bounds; ++i)
+        if (a.bidx[i] == t % n) {
+          const double xc = fmin(fmax(xv, a.blb[i]), a.bub[i]);
+          if (xc != xv) step = xc - Xs[t];
+          xv = xc;
+        }
+      dmax = isfinite(dv) ? fmax(dmax, fabs(step)) : INFINITY;
+      xmax = fmax(xmax, fabs(xv));
     }
-    double fin = finite ? 0.0 : 1.0;
-    block_reduce2(RED, dmax, fin, true);
-    if (fin != 0.0) {
+    block_reduce2(RED, dmax, xmax, true);
+    if (dmax == INFINITY) {
       status = MHE_STATUS_NONFINITE;
       break;
     }
     for (int t = tid_u; t < a.d; t += NTHREADS) {
-      const double xv = Xs[t] + DV[t];
+      double xv = Xs[t] + DV[t];
+      for (int i = 0; i < a.n_bounds; ++i)
+        if (a.bidx[i] == t % n) xv = fmin(fmax(xv, a.blb[i]), a.bub[i]);
       Xs[t] = xv;
-      xmax = fmax(xmax, fabs(xv));
     }
-    double dummy = 0.0;
-    block_reduce2(RED, xmax, dummy, true);
+    __syncthreads();
     ++it;
     if (dmax <= a.tol * (1.0 + xmax)) {
       status = MHE_STATUS_CONVERGED;
       // final cost at the converged iterate
-      double cf = node_phase<DYN>(a, CL, SL, sm, b);
+      double cf = node_phase<DYN, HUBER>(a, CL, SL, sm, b);
       cf += meas_phase<DYN, MEAS>(a, CL, SL, sm, b);
       __syncthreads();
       cf += grad_phase<DYN>(a, CL, SL, sm, b);
@@ -998,7 +1041,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void k_gn(GnArgs a) {
   {
     // cost at the returned iterate (the loop's last residual pass is at Xs
     // unless the iteration broke before updating)
-    double cf = node_phase<DYN>(a, CL, SL, sm, b);
+    double cf = node_phase<DYN, HUBER>(a, CL, SL, sm, b);
     cf += meas_phase<DYN, MEAS>(a, CL, SL, sm, b);
     __syncthreads();
     cf += grad_phase<DYN>(a, CL, SL, sm, b);
@@ -1020,7 +1063,7 @@ done:
 // ------------------------------------------------------------ constants
 // Cc tile element (row, col) of the constant part of J^T W J.
 template <class MEAS>
-__global__ void k_build_cc(int P, int M, int n, int p, int NT, int has_prior, double alpha,
+__global__ void k_build_cc(int P, int M, int n, int p, int NT, int has_prior, int huber, double alpha,
                            const double* D, const double* cw, const double* Phi, const double* Qw,
                            const double* Rw, const double* Pw, char* cbuf) {
   const ConstLayout CL = const_layout(P, M, n, p, NT);
@@ -1043,7 +1086,7 @@ __global__ void k_build_cc(int P, int M, int n, int p, int NT, int has_prior, do
     const int j = row / n, a = row % n, l = col / n, bb = col % n;
     double dcd = 0.0;
     for (int k = 0; k < P; ++k) dcd += D[k * P + j] * cw[k] * D[k * P + l];
-    v = alpha * alpha * dcd * Qw[a * n + bb];
+    v = huber ? 0.0 : alpha * alpha * dcd * Qw[a * n + bb];  // Huber: rebuilt per iteration
     if (MEAS::LINEAR) {  // full_state: H_i = I, G_i = Rw_i
       double s = 0.0;
       for (int i = 0; i < M; ++i) s += Phi[i * P + j] * Phi[i * P + l] * Rw[(i * p + a) * p + bb];
@@ -1151,6 +1194,11 @@ int check_dims(const mhe_dims* dm, int* NT_out) {
   if (!meas_info(dm->meas_model, n, p, q, lin)) return MHE_ERR_MODEL;
   if (dm->n != n || dm->m != m || dm->p != p || dm->q != q) return MHE_ERR_DIMS;
   if (dm->N < 1 || dm->M < 0 || !(dm->T > 0.0)) return MHE_ERR_DIMS;
+  if (dm->dyn_cost != MHE_COST_L2 && dm->dyn_cost != MHE_COST_HUBER) return MHE_ERR_MODEL;
+  if (dm->dyn_cost == MHE_COST_HUBER && !(dm->huber_delta > 0.0)) return MHE_ERR_DIMS;
+  if (dm->n_bounds < 0 || dm->n_bounds > 8) return MHE_ERR_DIMS;
+  for (int i = 0; i < dm->n_bounds; ++i)
+    if (dm->bound_idx[i] < 0 || dm->bound_idx[i] >= n || !(dm->bound_lb[i] <= dm->bound_ub[i])) return MHE_ERR_DIMS;
   if (dm->meas_model == MHE_MEAS_VEHICLE_PSEUDORANGE && n < 9) return MHE_ERR_DIMS;
   for (int i = 0; i < 4; ++i)
     if ((dm->meas_model == MHE_MEAS_PSEUDORANGE && (dm->meas_idx[i] < 0 || dm->meas_idx[i] >= n)) ||
@@ -1176,8 +1224,10 @@ int launch_gn(const mhe_dims* dm, GnArgs& a, int batch, int mode, hipStream_t st
   if (const char* pad = getenv("MHE_DEBUG_SMEM_PAD")) smem += atoi(pad);  // debug: force occupancy
   if (smem > 160 * 1024) return MHE_ERR_UNSUPPORTED;
   void (*kern)(GnArgs) = nullptr;
-  if (mode == MODE_SOLVE) kern = k_gn<DYN, MEAS, MAX_SLOTS, MODE_SOLVE>;
-  else if (mode == MODE_ASSEMBLE) kern = k_gn<DYN, MEAS, MAX_SLOTS, MODE_ASSEMBLE>;
+  const bool huber = dm->dyn_cost == MHE_COST_HUBER;
+  if (mode == MODE_SOLVE) kern = huber ? k_gn<DYN, MEAS, MAX_SLOTS, MODE_SOLVE, true> : k_gn<DYN, MEAS, MAX_SLOTS, MODE_SOLVE>;
+  else if (mode == MODE_ASSEMBLE)
+    kern = huber ? k_gn<DYN, MEAS, MAX_SLOTS, MODE_ASSEMBLE, true> : k_gn<DYN, MEAS, MAX_SLOTS, MODE_ASSEMBLE>;
   else kern = k_gn<DYN, MEAS, MAX_SLOTS, MODE_LINSOLVE>;
   if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem) != hipSuccess)
     return MHE_ERR_HIP;
@@ -1203,7 +1253,8 @@ int launch_cc(const mhe_dims* dm, int NT, const double* D, const double* cw, con
   hipLaunchKernelGGL(k_copy_consts, dim3(256), dim3(256), 0, st, P, dm->M, dm->n, dm->p, NT, D, cw, Phi, Qw,
                      Rw, Pw, cbuf);
   hipLaunchKernelGGL(k_build_cc<MEAS>, dim3((ntiles * 256 + 255) / 256), dim3(256), 0, st, P, dm->M, dm->n,
-                     dm->p, NT, dm->has_prior, 2.0 / dm->T, D, cw, Phi, Qw, Rw, Pw, cbuf);
+                     dm->p, NT, dm->has_prior, dm->dyn_cost == MHE_COST_HUBER ? 1 : 0, 2.0 / dm->T, D, cw, Phi,
+                     Qw, Rw, Pw, cbuf);
   return hipGetLastError() == hipSuccess ? MHE_OK : MHE_ERR_HIP;
 }
 
@@ -1253,6 +1304,13 @@ GnArgs make_args(const mhe_dims* dm, const void* cbuf, int NT) {
   a.has_prior = dm->has_prior;
   for (int i = 0; i < 8; ++i) a.idx[i] = dm->meas_idx[i];
   a.alpha = 2.0 / dm->T;
+  a.huber_delta = dm->huber_delta;
+  a.n_bounds = dm->n_bounds;
+  for (int i = 0; i < 8; ++i) {
+    a.bidx[i] = dm->bound_idx[i];
+    a.blb[i] = dm->bound_lb[i];
+    a.bub[i] = dm->bound_ub[i];
+  }
   return a;
 }
 
@@ -1377,6 +1435,7 @@ int mhe_gn_solve_ws(const mhe_dims* dims, const void* const_buf, int32_t batch, 
       (dims->m > 0 && !U) || (dims->q > 0 && !PAR) || (dims->has_prior && !x0))
     return MHE_ERR_NULL;
   if (is_big(dims)) {
+    if (dims->dyn_cost != MHE_COST_L2) return MHE_ERR_UNSUPPORTED;  // Huber: fused path only (this build)
     if (!workspace || workspace_bytes < mhe_workspace_bytes(dims, batch)) return MHE_ERR_NULL;
     BigArgs A = {};
     A.cbuf = (const char*)const_buf;
@@ -1387,6 +1446,12 @@ int mhe_gn_solve_ws(const mhe_dims* dims, const void* const_buf, int32_t batch, 
     A.U = U; A.ustride = u_bstride; A.Y = Y; A.PAR = PAR; A.pstride = par_bstride; A.x0 = x0;
     A.X = X_out; A.cost = cost_out; A.iters = iters_out; A.state = status_out; A.tol = tol;
     A.ws = (double*)workspace; A.ws_stride = big_ws_doubles(dims, NT);
+    A.n_bounds = dims->n_bounds;
+    for (int i = 0; i < 8; ++i) {
+      A.bidx[i] = dims->bound_idx[i];
+      A.blb[i] = dims->bound_lb[i];
+      A.bub[i] = dims->bound_ub[i];
+    }
     LaunchBig f{dims, &A, batch, max_iter, X0, (hipStream_t)stream};
     return dispatch(dims, f);
   }

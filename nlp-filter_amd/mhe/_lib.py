@@ -24,6 +24,8 @@ class MheDims(ctypes.Structure):
         ("N", c_i32), ("n", c_i32), ("m", c_i32), ("p", c_i32), ("M", c_i32), ("q", c_i32),
         ("dyn_model", c_i32), ("meas_model", c_i32), ("has_prior", c_i32),
         ("meas_idx", c_i32 * 8), ("T", c_dbl),
+        ("dyn_cost", c_i32), ("n_bounds", c_i32), ("huber_delta", c_dbl),
+        ("bound_idx", c_i32 * 8), ("bound_lb", c_dbl * 8), ("bound_ub", c_dbl * 8),
     ]
 
 

@@ -54,9 +54,12 @@ class BatchSolver:
       Rw (M,p,p)      measurement information (R passed to addResidualCost)
       Pw (n,n)|None   prior information (addInitialCost), None = no prior
       meas_idx        static index parameters of the measurement model
+      dyn_cost        "l2" (weighted_l2_norm) or "huber" (pseudo_huber_loss, IRLS; huber_delta)
+      bounds          [(state component, lb, ub), ...] enforced by projected GN (addVarBounds)
     """
 
-    def __init__(self, N, T, dyn, meas, D, cw, Phi, Qw, Rw, Pw=None, meas_idx=None, device="cuda"):
+    def __init__(self, N, T, dyn, meas, D, cw, Phi, Qw, Rw, Pw=None, meas_idx=None, device="cuda",
+                 dyn_cost="l2", huber_delta=None, bounds=None):
         self.lib = _lib.load()
         if not torch.cuda.is_available():
             raise _lib.MheLibraryError("no HIP device visible: the estimator has no CPU path")
@@ -78,6 +81,19 @@ class BatchSolver:
         for i in range(8):
             dims.meas_idx[i] = idx[i] if i < len(idx) else 0
         dims.T = self.T
+        if dyn_cost not in ("l2", "huber"):
+            raise ValueError(f"dyn_cost must be 'l2' or 'huber', got {dyn_cost!r}")
+        dims.dyn_cost = 1 if dyn_cost == "huber" else 0
+        dims.huber_delta = float(huber_delta) if huber_delta is not None else 0.0
+        bounds = list(bounds or [])
+        if len(bounds) > 8:
+            raise ValueError("at most 8 bounded state components")
+        dims.n_bounds = len(bounds)
+        for i, (c, lo, hi) in enumerate(bounds):
+            dims.bound_idx[i] = int(c)
+            dims.bound_lb[i] = -np.inf if lo is None else float(lo)
+            dims.bound_ub[i] = np.inf if hi is None else float(hi)
+        self.dyn_cost, self.huber_delta, self.bounds = dyn_cost, huber_delta, bounds
         self.dims = dims
         self.dp = self.lib.mhe_padded_dim(dims)
         if self.dp < 0:
@@ -199,8 +215,8 @@ class BatchSolver:
         return delta, status
 
 
-def from_workload(w, device="cuda"):
-    """BatchSolver for a mhe.configs.Workload."""
+def from_workload(w, device="cuda", **kw):
+    """BatchSolver for a mhe.configs.Workload (kw: dyn_cost, huber_delta, bounds)."""
     Phi = w.cpm.lagrange_matrix(w.t_meas)
     return BatchSolver(w.N, w.T, w.dyn, w.meas, w.cpm.D, (w.T / 2.0) * w.cpm.w, Phi, w.Qw, w.Rw,
-                       Pw=w.Pw, meas_idx=w.meas_static.get("idx"), device=device)
+                       Pw=w.Pw, meas_idx=w.meas_static.get("idx"), device=device, **kw)

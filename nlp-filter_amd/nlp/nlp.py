@@ -20,11 +20,14 @@ Kept semantics
   * ``extractVariableValue`` / ``extractSolution`` print and return None on a
     missing name or before ``solve()`` (nlp/nlp.py:85-119)
 
+  * ``pseudo_huber_loss`` dynamics cost (cost_functions.py:25-31) -> IRLS on the GPU
+  * ``addVarBounds`` on the state trajectory -> projected Gauss-Newton (steps are
+    clipped to the box); bounds on other variables are checked after the solve
+    (``self.solver["bounds_violated"]``)
+
 Not on the Gauss-Newton path yet (raise ``UnsupportedFeature``): inequality /
-equality constraints, the pseudo-Huber cost (f2), mixed
-measurement models in one problem, and ``fixedTimeOptimalControlNLP`` (out of
-scope: the north star is the estimator).  ``addVarBounds`` is recorded and
-checked after the solve (``self.solver["bounds_violated"]``) but not enforced.
+equality constraints, mixed measurement models in one problem,
+and ``fixedTimeOptimalControlNLP`` (out of scope: the north star is the estimator).
 """
 import time
 import warnings
@@ -194,13 +197,18 @@ class fixedTimeOptimalEstimationNLP(NLP):
     def addDynamicsCost(self, cost_function, W, params=None):
         """nlp/nlp.py:242-245: sum_k (T/2) w_k c(W_k)."""
         name = _fname(cost_function)
+        self._huber = None
         if name == "weighted_l2_norm":
             Qw = np.asarray(_resolve(params["Q"]), dtype=np.float64).reshape(self.n, self.n)
         elif name == "l2_norm":
             Qw = np.eye(self.n)
+        elif name == "pseudo_huber_loss":
+            # cost_functions.py:25-31: only diag(Q) enters; solved by IRLS on the GPU
+            Qw = np.asarray(_resolve(params["Q"]), dtype=np.float64).reshape(self.n, self.n)
+            self._huber = float(_resolve(params["delta"]))
         else:
-            raise UnsupportedFeature(f"dynamics cost {name!r}: the Gauss-Newton path needs a least-squares "
-                                     "cost (weighted_l2_norm / l2_norm); pseudo_huber_loss is SURVEY.md §8 f2")
+            raise UnsupportedFeature(f"dynamics cost {name!r}: supported are weighted_l2_norm, l2_norm and "
+                                     "pseudo_huber_loss")
         self._dyn_cost = Qw
 
     def addResidualCost(self, measurement_model, X, t_array, y_array, R, params=None):
@@ -248,8 +256,24 @@ class fixedTimeOptimalEstimationNLP(NLP):
             self.setParameter(Y[i], np.asarray(y_array)[:, i])
 
     def addVarBounds(self, X, idx, lb, ub):
-        """Recorded and checked after solve(); not enforced."""
+        """nlp/nlp.py:314-317.  Bounds on a component of the state trajectory are
+        enforced by projected Gauss-Newton (every step is clipped to the box);
+        bounds on other variables are recorded and checked after solve()."""
         self._bounds.append((X, idx, lb, ub))
+
+    def _enforced_bounds(self):
+        """(component, lb, ub) for bounds on the state variables, intersected per component."""
+        box = {}
+        for X, idx, lb, ub in self._bounds:
+            if self._X is None or (X is not self._X and list(X) != list(self._X)):
+                continue  # not the state trajectory: recorded and checked only
+            comps = list(range(self.n)) if idx is None else [int(idx)]
+            lbv = np.broadcast_to(np.asarray(-np.inf if lb is None else lb, dtype=np.float64).reshape(-1), (len(comps),))
+            ubv = np.broadcast_to(np.asarray(np.inf if ub is None else ub, dtype=np.float64).reshape(-1), (len(comps),))
+            for c, lo, hi in zip(comps, lbv, ubv):
+                plo, phi = box.get(c, (-np.inf, np.inf))
+                box[c] = (max(plo, float(lo)), min(phi, float(hi)))
+        return [(c, lo, hi) for c, (lo, hi) in sorted(box.items()) if np.isfinite(lo) or np.isfinite(hi)]
 
     # ------------------------------------------------------------ assembly
     def _spec(self):
@@ -291,10 +315,14 @@ class fixedTimeOptimalEstimationNLP(NLP):
         func = self._dyn[0]
         Phi = self.CPM.lagrange_matrix(t_meas)
         Pw = None if self._prior is None else np.asarray(_resolve(self._prior[0]), dtype=np.float64)
-        key = (Rw.tobytes(), None if Pw is None else Pw.tobytes(), self._dyn_cost.tobytes())
+        bounds = self._enforced_bounds()
+        huber = getattr(self, "_huber", None)
+        key = (Rw.tobytes(), None if Pw is None else Pw.tobytes(), self._dyn_cost.tobytes(), huber, tuple(bounds))
         if self._engine is None or self._engine_key != key:
             self._engine = _solver.BatchSolver(self.N, self.T, func, mname, self.CPM.D, (self.T / 2.0) * self.CPM.w,
-                                               Phi, self._dyn_cost, Rw, Pw=Pw, meas_idx=idx, device=self.device)
+                                               Phi, self._dyn_cost, Rw, Pw=Pw, meas_idx=idx, device=self.device,
+                                               dyn_cost="huber" if huber is not None else "l2", huber_delta=huber,
+                                               bounds=bounds)
             self._engine_key = key
         self._PAR = PAR
 
@@ -359,5 +387,5 @@ class fixedTimeOptimalEstimationNLP(NLP):
                 if ub is not None and np.any(v > np.asarray(ub) + 1e-9):
                     viol = True
         if viol:
-            warnings.warn("solution violates a recorded variable bound (bounds are not enforced yet)")
+            warnings.warn("solution violates a recorded variable bound (only state-trajectory bounds are enforced)")
         return viol

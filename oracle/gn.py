@@ -11,6 +11,11 @@ with the process-noise variables W eliminated through the collocation equality:
 
 Gauss-Newton on J (the same stationary point IPOPT returns for this
 unconstrained problem): H delta = -g with H = sum A^T W A, g = sum A^T W r.
+With the pseudo-Huber dynamics cost (cost_functions.py:25-31) the step is IRLS:
+per defect component W r -> rho'(r)/2 and W -> diag(rho'(r)/(2r)).
+With addVarBounds (nlp/nlp.py:314-317) the step is projected onto the box
+(projected Gauss-Newton; IPOPT's interior point reaches the same point when the
+bounds are inactive).
 
 Two independent forms are provided:
   * ``normal_equations``          structured (Kronecker) form, vectorised over the batch
@@ -28,8 +33,15 @@ OK, MAXITER, NOT_SPD, NONFINITE = 0, 1, 2, 3
 class Problem:
     """Structure shared by every trajectory of a batch (plain container)."""
 
-    def __init__(self, N, T, n, m, dyn, meas, D, c, Phi, Qw, Rw, Pw=None, meas_static=None):
+    def __init__(self, N, T, n, m, dyn, meas, D, c, Phi, Qw, Rw, Pw=None, meas_static=None,
+                 dyn_cost="l2", delta=None, lb=None, ub=None):
         self.N, self.T, self.n, self.m = N, float(T), n, m
+        # dynamics cost: "l2" = weighted_l2_norm, "huber" = pseudo_huber_loss with params
+        # {"Q": Qw, "delta": delta} (cost_functions.py:20-31; only diag(Qw) enters the Huber)
+        self.dyn_cost, self.delta = dyn_cost, None if delta is None else float(delta)
+        # addVarBounds (nlp/nlp.py:314-317) per state component: (n,) arrays, +-inf = free
+        self.lb = None if lb is None else np.asarray(lb, dtype=np.float64)
+        self.ub = None if ub is None else np.asarray(ub, dtype=np.float64)
         self.P = N + 1
         self.d = self.P * n
         self.alpha = 2.0 / float(T)
@@ -50,7 +62,11 @@ def residuals(pb, X, U, Y, PAR=None, x0=None):
     DX = np.einsum("kj,bja->bka", pb.D, X)
     f, _ = models.dyn_eval(pb.dyn, X, U)
     W = pb.alpha * DX - f
-    cost = np.einsum("k,bka,ac,bkc->b", pb.c, W, pb.Qw, W)
+    if pb.dyn_cost == "huber":  # sum_i 2 Q_ii delta^2 (sqrt(1 + W_i^2/delta^2) - 1), cost_functions.py:25-31
+        q, dl = np.diag(pb.Qw), pb.delta
+        cost = np.einsum("k,bka->b", pb.c, 2.0 * q * dl ** 2 * (np.sqrt(1.0 + W ** 2 / dl ** 2) - 1.0))
+    else:
+        cost = np.einsum("k,bka,ac,bkc->b", pb.c, W, pb.Qw, W)
     xi = np.einsum("ij,bja->bia", pb.Phi, X)
     h, _ = models.meas_eval(pb.meas, xi, PAR, pb.meas_static)
     e = Y - h
@@ -70,15 +86,24 @@ def normal_equations(pb, X, U, Y, PAR=None, x0=None):
     _, F = models.dyn_eval(pb.dyn, X, U)
     a = pb.alpha
     # dynamics: block(j,l) = a^2 (D^T C D)_jl Qw - a D_lj E_l - a D_jl E_j^T + delta_jl F_j^T E_j
-    E = np.einsum("k,ac,zkce->zkae", pb.c, pb.Qw, F)              # c_k Qw F_k
-    DCD = np.einsum("kj,k,kl->jl", pb.D, pb.c, pb.D)
-    H4 = np.broadcast_to((a * a) * np.einsum("jl,ae->jale", DCD, pb.Qw), (B, P, n, P, n)).copy()
+    if pb.dyn_cost == "huber":
+        # IRLS: the half-gradient Qw W -> rho'(W)/2, the weight Qw -> diag(rho'(W)/(2W))
+        Lam, Vh = huber_weights(pb, W)                           # (B,P,n) each
+        E = pb.c[None, :, None, None] * Lam[..., None] * F        # c_k diag(Lam_k) F_k
+        H4 = (a * a) * np.einsum("kj,k,kl,zka,ae->zjale", pb.D, pb.c, pb.D, Lam, np.eye(n))
+    else:
+        E = np.einsum("k,ac,zkce->zkae", pb.c, pb.Qw, F)          # c_k Qw F_k
+        DCD = np.einsum("kj,k,kl->jl", pb.D, pb.c, pb.D)
+        H4 = np.broadcast_to((a * a) * np.einsum("jl,ae->jale", DCD, pb.Qw), (B, P, n, P, n)).copy()
     H4 -= a * np.einsum("lj,zlae->zjale", pb.D, E)
     H4 -= a * np.einsum("jl,zjea->zjale", pb.D, E)
     FtE = np.einsum("zjca,zjce->zjae", F, E)
     for j in range(P):
         H4[:, j, :, j, :] += FtE[:, j]
-    V = np.einsum("k,ac,zkc->zka", pb.c, pb.Qw, W)                # c_k Qw W_k
+    if pb.dyn_cost == "huber":
+        V = pb.c[None, :, None] * Vh                              # c_k rho'(W_k)/2
+    else:
+        V = np.einsum("k,ac,zkc->zka", pb.c, pb.Qw, W)            # c_k Qw W_k
     g = a * np.einsum("kj,zka->zja", pb.D, V) - np.einsum("zjca,zjc->zja", F, V)
     # measurements
     _, Hm = models.meas_eval(pb.meas, xi, PAR, pb.meas_static)    # (B,M,p,n)
@@ -92,6 +117,16 @@ def normal_equations(pb, X, U, Y, PAR=None, x0=None):
         g[:, 0] += (X[:, 0] - x0) @ pb.Pw.T
     d = P * n
     return H4.reshape(B, d, d), g.reshape(B, d), cost
+
+
+def huber_weights(pb, W):
+    """Per-component pseudo-Huber IRLS weights at the defects W (B,P,n):
+    Lam = rho'(W) / (2 W) = q / sqrt(1 + W^2/delta^2),  Vh = rho'/2 = Lam W.
+    (IRLS majorises the loss, so undamped steps decrease it monotonically; the
+    fixed point is the stationary point of the pseudo-Huber objective.)"""
+    q, dl = np.diag(pb.Qw), pb.delta
+    lam = q / np.sqrt(1.0 + W ** 2 / dl ** 2)
+    return lam, lam * W
 
 
 def normal_equations_explicit(pb, X, U, Y, PAR=None, x0=None):
@@ -109,6 +144,13 @@ def normal_equations_explicit(pb, X, U, Y, PAR=None, x0=None):
             for j in range(P):
                 A[:, j * n:(j + 1) * n] += pb.alpha * pb.D[k, j] * np.eye(n)
             A[:, k * n:(k + 1) * n] -= Fk
+            if pb.dyn_cost == "huber":  # IRLS: H += A^T diag(c rho'/(2W)) A, g += A^T (c rho'/2)
+                q, dl = np.diag(pb.Qw), pb.delta
+                sk = 1.0 + Wk ** 2 / dl ** 2
+                lam = pb.c[k] * q / np.sqrt(sk)
+                rows.append(A); Ws.append(np.diag(lam)); rs.append(("g", lam * Wk,
+                                                                    pb.c[k] * np.sum(2 * q * dl ** 2 * (np.sqrt(sk) - 1))))
+                continue
             rows.append(A); Ws.append(pb.c[k] * pb.Qw); rs.append(Wk)
         Rw = pb.Rw[b] if pb.Rw.ndim == 4 else pb.Rw
         for i in range(pb.M):  # measurement rows, nlp/nlp.py:264-273
@@ -125,6 +167,10 @@ def normal_equations_explicit(pb, X, U, Y, PAR=None, x0=None):
         H = np.zeros((d, d)); g = np.zeros(d); c = 0.0
         for A, Wm, r in zip(rows, Ws, rs):
             H += A.T @ Wm @ A
+            if isinstance(r, tuple):  # (tag, weighted half-gradient, cost) for non-quadratic costs
+                g += A.T @ r[1]
+                c += r[2]
+                continue
             g += A.T @ (Wm @ r)
             c += r @ Wm @ r
         Hs.append(H); gs.append(g); cs.append(c)
@@ -164,9 +210,17 @@ def gauss_newton(pb, X0, U, Y, PAR=None, x0=None, max_iter=20, tol=1e-10):
                 status[b] = NONFINITE
                 active[b] = False
                 continue
-            X[b] += delta.reshape(X.shape[1:])
+            step = delta.reshape(X.shape[1:])
+            xn = X[b] + step
+            if pb.lb is not None or pb.ub is not None:  # projected step (addVarBounds)
+                lo = -np.inf if pb.lb is None else pb.lb
+                hi = np.inf if pb.ub is None else pb.ub
+                xc = np.minimum(np.maximum(xn, lo), hi)
+                step = np.where(xc != xn, xc - X[b], step)
+                xn = xc
+            X[b] = xn
             iters[b] += 1
-            if np.max(np.abs(delta)) <= tol * (1.0 + np.max(np.abs(X[b]))):
+            if np.max(np.abs(step)) <= tol * (1.0 + np.max(np.abs(X[b]))):
                 status[b] = OK
                 active[b] = False
     _, _, _, cost = residuals(pb, X, U, Y, PAR, x0)

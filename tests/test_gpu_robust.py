@@ -1,0 +1,127 @@
+"""Pseudo-Huber dynamics cost (IRLS) and variable bounds (projected GN) on the GPU
+vs the CPU oracle (oracle/gn.py: same iteration -- cost_functions.py:25-31,
+nlp/nlp.py:314-317).
+
+Tolerances as tests/test_gpu_parity.py: assembled H, g <= 1e-12 relative; iterates
+<= 1e-9 (1 + max|X|) after the same number of iterations; converged <= 1e-8;
+bound satisfaction exact (the projection clips to the bound value).
+"""
+import os
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+from mhe import _lib, configs, solver  # noqa: E402
+from oracle import gn  # noqa: E402
+
+DELTA = 0.02
+
+
+def _pb(w, **kw):
+    return gn.Problem(w.N, w.T, w.n, w.m, w.dyn, w.meas, w.cpm.D, (w.T / 2) * w.cpm.w,
+                      w.cpm.lagrange_matrix(w.t_meas), w.Qw, w.Rw, Pw=w.Pw, meas_static=w.meas_static, **kw)
+
+
+def _U(w):
+    return np.broadcast_to(w.U, (w.B,) + w.U.shape[1:])
+
+
+def _np(ts):
+    return [t.cpu().numpy() for t in ts]
+
+
+def test_huber_assembly_matches_oracle():
+    w = configs.make_c2(B=3, N=20)
+    s = solver.from_workload(w, dyn_cost="huber", huber_delta=DELTA)
+    H, g, cost = _np(s.assemble(w.X_init, w.U, w.Y))
+    Hr, gr, cr = gn.normal_equations(_pb(w, dyn_cost="huber", delta=DELTA), w.X_init, _U(w), w.Y)
+    d = Hr.shape[1]
+    assert np.abs(H[:, :d, :d] - Hr).max() <= 1e-12 * np.abs(Hr).max()
+    assert np.abs(g[:, :d] - gr).max() <= 1e-12 * np.abs(gr).max()
+    assert np.allclose(cost, cr, rtol=1e-12)
+
+
+@pytest.mark.parametrize("max_iter,tol", [(5, 0.0), (400, 1e-10)])
+def test_huber_iterates_match_oracle(max_iter, tol):
+    w = configs.make_c2(B=4, N=20)
+    s = solver.from_workload(w, dyn_cost="huber", huber_delta=DELTA)
+    X, cost, iters, status = _np(s.solve(w.X_init, w.U, w.Y, max_iter=max_iter, tol=tol))
+    Xr, cr, ir, sr = gn.gauss_newton(_pb(w, dyn_cost="huber", delta=DELTA), w.X_init, _U(w), w.Y,
+                                     max_iter=max_iter, tol=tol)
+    assert status.tolist() == sr.tolist()
+    assert np.all(np.abs(iters - ir) <= (0 if tol == 0 else 1))
+    lim = 1e-9 if tol == 0 else 1e-8
+    assert np.abs(X - Xr).max() <= lim * (1 + np.abs(Xr).max())
+    assert np.allclose(cost, cr, rtol=lim)
+
+
+def _bounds_case():
+    w = configs.make_c2(B=4, N=20)
+    bounds = [(1, 0.5, np.inf), (0, -np.inf, 1.5)]
+    pb = _pb(w, lb=[-np.inf, 0.5], ub=[1.5, np.inf])
+    return w, bounds, pb
+
+
+def _check_bounds(w, X, cost, iters, status, pb):
+    Xr, cr, ir, sr = gn.gauss_newton(pb, w.X_init, _U(w), w.Y, max_iter=30, tol=1e-10)
+    assert (X[:, :, 1] >= 0.5).all() and (X[:, :, 0] <= 1.5).all()
+    assert (X[:, :, 1] == 0.5).any(), "the test bound should be active"
+    assert status.tolist() == sr.tolist() and np.all(np.abs(iters - ir) <= 1)
+    assert np.abs(X - Xr).max() <= 1e-8 * (1 + np.abs(Xr).max())
+    assert np.allclose(cost, cr, rtol=1e-8)
+
+
+def test_bounds_projected_gn_register_path():
+    w, bounds, pb = _bounds_case()
+    s = solver.from_workload(w, bounds=bounds)
+    _check_bounds(w, *_np(s.solve(w.X_init, w.U, w.Y, max_iter=30, tol=1e-10)), pb)
+
+
+def test_bounds_projected_gn_large_system_path():
+    w, bounds, pb = _bounds_case()
+    os.environ["MHE_FORCE_BIG"] = "1"
+    try:
+        s = solver.from_workload(w, bounds=bounds)
+        assert s.large_system
+        out = _np(s.solve(w.X_init, w.U, w.Y, max_iter=30, tol=1e-10))
+    finally:
+        os.environ.pop("MHE_FORCE_BIG", None)
+    _check_bounds(w, *out, pb)
+
+
+def test_huber_on_large_system_path_is_refused():
+    w = configs.make_c2(B=2, N=150)
+    s = solver.from_workload(w, dyn_cost="huber", huber_delta=DELTA)
+    with pytest.raises(_lib.MheCallError):
+        s.solve(w.X_init, w.U, w.Y, max_iter=2)
+
+
+def test_facade_huber_and_bounds_match_oracle():
+    """nlp.NLP path: addDynamicsCost(pseudo_huber_loss) + addVarBounds, as autonomous-car.py."""
+    import nlp.cost_functions as cost_functions
+    import nlp.dynamics as dynamics
+    import nlp.measurements as measurements
+    import nlp.nlp as nlp
+    w = configs.make_c2(B=1, N=20)
+    Q = np.linalg.inv(w.Qw)
+    problem = nlp.fixedTimeOptimalEstimationNLP(w.N, w.T, w.n, w.m)
+    X = problem.addVariables(w.N + 1, w.n, name="x")
+    t_nodes = w.cpm.tau2t(w.cpm.tau)
+    problem.addDynamics(dynamics.van_der_pol, X, t_nodes, np.zeros((1, w.N + 1)))
+    problem.addDynamicsCost(cost_functions.pseudo_huber_loss, None, {"Q": np.linalg.inv(Q), "delta": DELTA})
+    problem.addResidualCost(measurements.full_state, X, w.t_meas, w.Y[0].T, w.Rw[0])
+    problem.addVarBounds(X, 1, 0.5, np.inf)
+    problem.initializeEstimate(X, t_nodes, w.X_init[0].T)
+    problem.max_iter, problem.tol = 40, 0.0  # same iteration count on both sides (projected IRLS)
+    problem.solve()
+    Xg = np.stack([problem.extractVariableValue("x", k) for k in range(w.N + 1)])
+    pb = _pb(w, dyn_cost="huber", delta=DELTA, lb=[-np.inf, 0.5], ub=[np.inf, np.inf])
+    Xr, cr, ir, sr = gn.gauss_newton(pb, w.X_init, _U(w), w.Y, max_iter=40, tol=0.0)
+    assert problem.solver["iter_count"] == ir[0] == 40
+    assert (Xg[:, 1] >= 0.5).all() and not problem.solver["bounds_violated"]
+    assert np.abs(Xg - Xr[0]).max() <= 1e-8 * (1 + np.abs(Xr).max())
+    assert np.isclose(problem.solver["objective"], cr[0], rtol=1e-8)

@@ -43,7 +43,7 @@ def test_soft_errors_and_unsupported():
     with pytest.raises(nlp.UnsupportedFeature):
         problem.addEqConstraint(lambda a, p: a[0] - a[1], [X[0], X[1]])
     with pytest.raises(nlp.UnsupportedFeature):
-        problem.addDynamicsCost(cost_functions.pseudo_huber_loss, None, {"Q": np.eye(1), "delta": 1.0})
+        problem.addDynamicsCost(lambda x, params=None: x, None, {"Q": np.eye(1)})  # not a registered cost
     with pytest.raises(nlp.UnsupportedFeature):
         nlp.fixedTimeOptimalControlNLP(10, 1.0, 2, 1)
 

@@ -67,3 +67,57 @@ def test_gn_optimum_is_stationary_fd():
     g0 = fd_grad(w.X_init[0].ravel())
     gs = fd_grad(X[0].ravel())
     assert np.abs(gs).max() <= 1e-6 * np.abs(g0).max()
+
+
+def _huber_problem(w, delta=0.05, lb=None, ub=None):
+    return gn.Problem(w.N, w.T, w.n, w.m, w.dyn, w.meas, w.cpm.D, (w.T / 2) * w.cpm.w,
+                      w.cpm.lagrange_matrix(w.t_meas), w.Qw, w.Rw, Pw=w.Pw, meas_static=w.meas_static,
+                      dyn_cost="huber", delta=delta, lb=lb, ub=ub)
+
+
+def test_huber_structured_equals_explicit():
+    w = configs.make_c2(B=2, N=20)
+    pb = _huber_problem(w)
+    U = np.broadcast_to(w.U, (w.B,) + w.U.shape[1:])
+    H1, g1, c1 = gn.normal_equations(pb, w.X_init, U, w.Y)
+    H2, g2, c2 = gn.normal_equations_explicit(pb, w.X_init, U, w.Y)
+    assert np.abs(H1 - H2).max() <= 1e-13 * np.abs(H2).max()
+    assert np.abs(g1 - g2).max() <= 1e-12 * np.abs(g2).max()
+    assert np.allclose(c1, c2, rtol=1e-13)
+
+
+def test_huber_gn_optimum_is_stationary_fd():
+    """The IRLS fixed point is a stationary point of the pseudo-Huber objective
+    (cost_functions.py:25-31): central-difference gradient ~ 0."""
+    w = configs.make_c2(B=1, N=15)
+    pb = _huber_problem(w, delta=0.02)
+    U = np.broadcast_to(w.U, (1,) + w.U.shape[1:])
+    X, cost, iters, status = gn.gauss_newton(pb, w.X_init, U, w.Y, max_iter=400, tol=1e-10)
+    assert status[0] == gn.OK  # IRLS: linear convergence (~110 iterations here)
+    x = X.ravel()
+    grad = np.zeros_like(x)
+    h = 1e-6
+    for i in range(x.size):
+        xp, xm = x.copy(), x.copy()
+        xp[i] += h
+        xm[i] -= h
+        grad[i] = (gn.residuals(pb, xp.reshape(X.shape), U, w.Y)[3][0] -
+                   gn.residuals(pb, xm.reshape(X.shape), U, w.Y)[3][0]) / (2 * h)
+    _, g, _ = gn.normal_equations(pb, X, U, w.Y)
+    assert np.abs(grad).max() <= 1e-5 * max(1.0, cost[0])
+    assert np.abs(2 * g[0]).max() <= 1e-7 * max(1.0, cost[0])
+
+
+def test_projected_bounds_respected_and_inactive_bounds_change_nothing():
+    w = configs.make_c2(B=2, N=20)
+    U = np.broadcast_to(w.U, (w.B,) + w.U.shape[1:])
+    free = _problem(w)
+    Xf, cf, itf, sf = gn.gauss_newton(free, w.X_init, U, w.Y, max_iter=30, tol=1e-10)
+    loose = gn.Problem(w.N, w.T, w.n, w.m, w.dyn, w.meas, w.cpm.D, (w.T / 2) * w.cpm.w,
+                       w.cpm.lagrange_matrix(w.t_meas), w.Qw, w.Rw, lb=[-10, -10], ub=[10, 10])
+    Xl, cl, itl, sl = gn.gauss_newton(loose, w.X_init, U, w.Y, max_iter=30, tol=1e-10)
+    assert np.array_equal(Xl, Xf) and np.array_equal(itl, itf)
+    tight = gn.Problem(w.N, w.T, w.n, w.m, w.dyn, w.meas, w.cpm.D, (w.T / 2) * w.cpm.w,
+                       w.cpm.lagrange_matrix(w.t_meas), w.Qw, w.Rw, lb=[-np.inf, 0.5], ub=[np.inf, np.inf])
+    Xt, ct, itt, st = gn.gauss_newton(tight, w.X_init, U, w.Y, max_iter=30, tol=1e-10)
+    assert (Xt[:, :, 1] >= 0.5).all() and (Xt[:, :, 1] == 0.5).any()
