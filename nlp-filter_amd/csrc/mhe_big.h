@@ -350,9 +350,10 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_chol(BigArgs a) {
       const double* Akk = H + (size_t)big_tile_index(k, k, NT) * 256;
       for (int e = lane; e < 256; e += 64) DT[e] = -Akk[e];
       wave_lds_sync();
-      const bool bad = panel(DT, BV + 16 * k, YV + 16 * k, lane);
+      const bool bad = panel(DT, lane);
       if (bad && lane == 0) *flag = 1;
       wave_lds_sync();
+      block_fwd(DT, BV + 16 * k, YV + 16 * k, lane);  // y_k = L_kk^-1 b_k
       for (int e = lane; e < DTS; e += 64) LTg[(size_t)k * DTS + e] = DT[e];
     }
     __syncthreads();

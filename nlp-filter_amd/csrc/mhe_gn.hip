@@ -29,7 +29,7 @@ namespace mhe {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
-constexpr int NW = 4;              // waves per workgroup (one trajectory)
+constexpr int NW = 8;              // waves per workgroup (one trajectory)
 constexpr int NTHREADS = NW * 64;
 constexpr int MAX_NT = 13;         // padded system <= 208 (register-resident path)
 // The NT(NT-1)/2 off-diagonal tiles live in MFMA accumulator registers (20
@@ -218,11 +218,11 @@ __device__ __forceinline__ int slot_start(int j, int wave, int NT) {
 }
 
 // ------------------------------------------------------------ model phases
-// Mat-vec phases use TPR = 2 threads per row: each sums half of the row with
-// an 8-deep unrolled loop (8 independent L2 loads in flight), the halves are
-// combined with one lane swap.  The tables (D, D^T, Phi, Phi^T) are shared by
-// every workgroup and L2-resident.
-constexpr int TPR = 2;
+// Mat-vec phases use TPR threads per row (4 with 8 waves): each sums every
+// TPR-th term of the row with an 8-deep unrolled loop (8 independent L2 loads
+// in flight), the parts are combined with lane swaps.  The tables (D, D^T, Phi,
+// Phi^T) are shared by every workgroup and L2-resident.
+constexpr int TPR = NW >= 8 ? 4 : 2;
 
 // threadIdx.x through an opaque move: values derived from it inside a phase
 // are recomputed per phase instead of being hoisted out of the Gauss-Newton
@@ -234,29 +234,31 @@ __device__ __forceinline__ int opaque_tid() {
 }
 
 template <int n>
-__device__ __forceinline__ void dot_rows_half(const double* __restrict__ Mt, int ld, int row, int len, int half,
+__device__ __forceinline__ void dot_rows_part(const double* __restrict__ Mt, int ld, int row, int len, int part,
                                               const double* __restrict__ Xs, double (&acc)[n]) {
-  // acc[c] = sum_{j = half, half+2, ...} Mt[j*ld + row] * Xs[j*n + c]
+  // acc[c] = sum_j Mt[j*ld + row] * Xs[j*n + c], summed over the TPR lanes of the row
 #pragma unroll
   for (int c = 0; c < n; ++c) acc[c] = 0.0;
-  int j = half;
+  int j = part;
 #pragma unroll 1
-  for (; j + 2 * 7 < len; j += 2 * 8) {
+  for (; j + TPR * 7 < len; j += TPR * 8) {
     double m[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) m[u] = Mt[(j + 2 * u) * ld + row];
+    for (int u = 0; u < 8; ++u) m[u] = Mt[(j + TPR * u) * ld + row];
 #pragma unroll
     for (int u = 0; u < 8; ++u)
 #pragma unroll
-      for (int c = 0; c < n; ++c) acc[c] += m[u] * Xs[(j + 2 * u) * n + c];
+      for (int c = 0; c < n; ++c) acc[c] += m[u] * Xs[(j + TPR * u) * n + c];
   }
-  for (; j < len; j += 2) {
+  for (; j < len; j += TPR) {
     const double mv = Mt[j * ld + row];
 #pragma unroll
     for (int c = 0; c < n; ++c) acc[c] += mv * Xs[j * n + c];
   }
 #pragma unroll
-  for (int c = 0; c < n; ++c) acc[c] += __shfl_xor(acc[c], 1);
+  for (int o = 1; o < TPR; o <<= 1)
+#pragma unroll
+    for (int c = 0; c < n; ++c) acc[c] += __shfl_xor(acc[c], o);
 }
 
 // Per-node dynamics quantities (nlp/nlp.py:225-245):
@@ -271,13 +273,13 @@ __device__ __forceinline__ double node_phase(const GnArgs& a, const ConstLayout&
   const double* Xs = sm + SL.Xs;
   double cost = 0.0;
   const int tid = opaque_tid();
-  const int half = tid & 1;
+  const int part = tid % TPR;
   for (int k0 = 0; k0 < a.P; k0 += NTHREADS / TPR) {
-    const int k = k0 + (tid >> 1);
+    const int k = k0 + tid / TPR;
     const int kk = k < a.P ? k : a.P - 1;
     double dx[n];
-    dot_rows_half<n>(Dt, a.P, kk, a.P, half, Xs, dx);
-    if (half || k >= a.P) continue;
+    dot_rows_part<n>(Dt, a.P, kk, a.P, part, Xs, dx);
+    if (part || k >= a.P) continue;
     double xk[n], uk[m > 0 ? m : 1], f[n], F[n * n];
 #pragma unroll
     for (int c = 0; c < n; ++c) xk[c] = Xs[k * n + c];
@@ -361,13 +363,13 @@ __device__ __forceinline__ double meas_phase(const GnArgs& a, const ConstLayout&
   const double* Xs = sm + SL.Xs;
   double cost = 0.0;
   const int tid = opaque_tid();
-  const int half = tid & 1;
+  const int part = tid % TPR;
   for (int i0 = 0; i0 < a.M; i0 += NTHREADS / TPR) {
-    const int i = i0 + (tid >> 1);
+    const int i = i0 + tid / TPR;
     const int ii = i < a.M ? i : a.M - 1;
     double xi[n];
-    dot_rows_half<n>(PhiT, a.M, ii, a.P, half, Xs, xi);
-    if (half || i >= a.M) continue;
+    dot_rows_part<n>(PhiT, a.M, ii, a.P, part, Xs, xi);
+    if (part || i >= a.M) continue;
     double par[q > 0 ? q : 1];
     if (q > 0) {
       const double* PR = a.PAR + (long long)b * a.pstride + (long long)i * q;
@@ -425,7 +427,7 @@ __device__ __forceinline__ double meas_phase(const GnArgs& a, const ConstLayout&
 
 // Gradient g = J^T W r (nlp/nlp.py:242-286 objective); writes BV = -g (padding 0).
 //   g_j = a sum_k D_kj V_k - F_j^T V_j - sum_i Phi_ij GE_i (+ Pw (X_0 - x0) at j = 0)
-// Thread pair per node: even lane sums the D column, odd lane the Phi column.
+// TPR lanes per node: half sum the D column, half the Phi column.
 template <class DYN>
 __device__ __forceinline__ double grad_phase(const GnArgs& a, const ConstLayout& CL, const SmemLayout& SL, double* sm, int b) {
   constexpr int n = DYN::n;
@@ -440,37 +442,44 @@ __device__ __forceinline__ double grad_phase(const GnArgs& a, const ConstLayout&
   double cost = 0.0;
   const int dp = 16 * a.NT;
   const int tid = opaque_tid();
-  const int odd = tid & 1;
+  // TPR lanes per node: the first half sums the D column (sum_k D[k][j] V_k), the
+  // second half the Phi column (sum_i Phi[i][j] GE_i), each split over TPR/2 lanes
+  constexpr int HP = TPR / 2;
+  const int q = tid % TPR, sub = q % HP;
+  const bool phi = q >= HP;
   for (int j0 = 0; j0 < a.P; j0 += NTHREADS / TPR) {
-    const int j = j0 + (tid >> 1);
+    const int j = j0 + tid / TPR;
     const int jj = j < a.P ? j : a.P - 1;
-    // even lane: sum_k D[k][j] V_k ; odd lane: sum_i Phi[i][j] GE_i
-    const double* Mt = odd ? Phi : D;
-    const double* vec = odd ? GE : Vs;
-    const int len = odd ? a.M : a.P;
+    const double* Mt = phi ? Phi : D;
+    const double* vec = phi ? GE : Vs;
+    const int len = phi ? a.M : a.P;
     double s[n];
 #pragma unroll
     for (int c = 0; c < n; ++c) s[c] = 0.0;
-    int k = 0;
+    int k = sub;
 #pragma unroll 1
-    for (; k + 7 < len; k += 8) {
+    for (; k + HP * 7 < len; k += HP * 8) {
       double mv[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) mv[u] = Mt[(k + u) * a.P + jj];
+      for (int u = 0; u < 8; ++u) mv[u] = Mt[(k + HP * u) * a.P + jj];
 #pragma unroll
       for (int u = 0; u < 8; ++u)
 #pragma unroll
-        for (int c = 0; c < n; ++c) s[c] += mv[u] * vec[(k + u) * n + c];
+        for (int c = 0; c < n; ++c) s[c] += mv[u] * vec[(k + HP * u) * n + c];
     }
-    for (; k < len; ++k) {
+    for (; k < len; k += HP) {
       const double mv = Mt[k * a.P + jj];
 #pragma unroll
       for (int c = 0; c < n; ++c) s[c] += mv * vec[k * n + c];
     }
+#pragma unroll
+    for (int o2 = 1; o2 < HP; o2 <<= 1)
+#pragma unroll
+      for (int c = 0; c < n; ++c) s[c] += __shfl_xor(s[c], o2);
     double o[n];
 #pragma unroll
-    for (int c = 0; c < n; ++c) o[c] = __shfl_xor(s[c], 1);
-    if (odd || j >= a.P) continue;
+    for (int c = 0; c < n; ++c) o[c] = __shfl_xor(s[c], HP);  // the other column's sum
+    if (q != 0 || j >= a.P) continue;
     double gv[n];
 #pragma unroll
     for (int c = 0; c < n; ++c) gv[c] = a.alpha * s[c] - FtV[j * n + c] - o[c];
@@ -639,38 +648,45 @@ __device__ __forceinline__ double row16_sum(double v) {
   return v;
 }
 
+// 1/sqrt(x) for a positive finite pivot: hardware v_rsq_f64 (~1e-9 relative)
+// refined by one Newton step (error squared: ~1 ulp).  Non-positive or
+// non-finite pivots are flagged by the caller and poison the factor anyway.
+__device__ __forceinline__ double rsqrt_pivot(double x) {
+  const double r = __builtin_amdgcn_rsq(x);
+  const double e = fma(-x * r, r, 1.0);  // 1 - x r^2
+  return fma(0.5 * r, e, r);
+}
+
 // Panel of block k, run by ONE wave (look-ahead: during the previous step's
-// trailing update).  On entry DT[k] holds the fully updated A_kk (row-major)
-// (negated, as all tiles) and bk the fully updated b_k.  One right-looking
-// elimination in which the
-// same register index j carries three things, one per lane role:
+// trailing update).  On entry DT[k] holds the fully updated A_kk (row-major,
+// negated as all tiles).  One right-looking elimination in which the same
+// register index j carries two things, one per lane role:
 //   lanes  0..15  row i of A_kk:              v[j] = A'_ij
 //   lanes 16..31  column t of the identity:   v[j] = E'_jt
-//   lane  32      the right-hand side:        v[j] = b'_j
 // Pivot c:  rs = 1 / sqrt(A'_cc);  q = v[c] rs  (= L_ic on row lanes, = (L^-1)_ct
-// and y_c on the others, which are final at that point);  then for j > c
+// on the others, final at that point);  then for j > c
 //   v[j] -= q L_jc   with L_jc = q of row lane j (v_readlane),
-// i.e. ONE fma updates the Cholesky trailing row, the forward substitution
-// L Y = I and L y = b together (~580 VALU instructions, ~40 VGPRs).
-// Stores L_kk^-T into DT[k] (row stride LIS) and y_k into yk.
+// i.e. ONE fma updates the Cholesky trailing row and the forward substitution
+// L Y = I together (~550 VALU instructions, ~40 VGPRs).  Stores L_kk^-T into
+// DT[k] (row stride LIS).  The right-hand side is NOT carried here: y_k =
+// L_kk^-1 b_k is formed later by another wave (off this critical chain).
 // Returns true if a pivot was not positive and finite (wave-uniform).
-__device__ __forceinline__ bool panel(double* DTk, const double* bk, double* yk, int lane) {
+__device__ __forceinline__ bool panel(double* DTk, int lane) {
   const int i = lane & 15;
   const bool erow = (lane >= 16 && lane < 32);
   double v[16];
 #pragma unroll
   for (int c = 0; c < 16; c += 2) {
     const double2 a2 = *(const double2*)(DTk + i * 16 + c);
-    const double2 b2 = *(const double2*)(bk + c);
-    v[c] = (lane == 32) ? b2.x : (erow ? (c == i ? 1.0 : 0.0) : -a2.x);  // DT holds -A_kk
-    v[c + 1] = (lane == 32) ? b2.y : (erow ? (c + 1 == i ? 1.0 : 0.0) : -a2.y);
+    v[c] = erow ? (c == i ? 1.0 : 0.0) : -a2.x;  // DT holds -A_kk
+    v[c + 1] = erow ? (c + 1 == i ? 1.0 : 0.0) : -a2.y;
   }
   bool bad = false;
 #pragma unroll
   for (int c = 0; c < 16; ++c) {
     const double piv = readlane_d(v[c], c);
     bad |= !(piv > 0.0 && piv < INFINITY);
-    const double q = v[c] * rsqrt(piv);
+    const double q = v[c] * rsqrt_pivot(piv);
     v[c] = q;
 #pragma unroll
     for (int j = c + 1; j < 16; ++j) v[j] -= q * readlane_d(q, j);
@@ -678,12 +694,14 @@ __device__ __forceinline__ bool panel(double* DTk, const double* bk, double* yk,
   if (erow) {
 #pragma unroll
     for (int j = 0; j < 16; ++j) DTk[i * LIS + j] = v[j];  // (L^-T)[t][j] = (L^-1)[j][t]
-  } else if (lane == 32) {
-#pragma unroll
-    for (int j = 0; j < 16; ++j) yk[j] = v[j];
   }
   return bad;
 }
+
+// y = L^-1 b for one block (L^-T stored with row stride LIS), by a whole wave:
+// lane (c, g = l >> 4) sums the terms s = 4g..4g+3 of row c of L^-1, i.e. column
+// c of L^-T, rows4_sum completes the dot.  Lanes 0..15 write y[c].
+__device__ __forceinline__ void block_fwd(const double* LT, const double* b, double* y, int lane);
 
 // Right-looking blocked Cholesky H = U^T U (U = L^T) with the forward solve
 // U^T y = b (b = -g in BV) fused.  Slot (I, J), I > J, holds the upper block
@@ -719,6 +737,8 @@ __device__ __forceinline__ bool factor_forward(const GnArgs& a, const SmemLayout
     // ---- T(k): U_kb = L_kk^-1 A_kb for the tiles (k, b) of this wave, slots [sT, sU)
     const int sT = slot_start(k < 0 ? 0 : k, wave_o, NT), sU = slot_start(k + 1, wave_o, NT);
     const int nS = slot_start(NT - 1, wave_o, NT);
+    if (k >= 0 && wave_o == (k + 2) % NW)  // forward solve, one block behind the factorization
+      block_fwd(DT + k * DTS, BV + 16 * k, YV + 16 * k, lane_o);
     if (k >= 0) {
       const double* LT = DT + k * DTS;
       double la[4];
@@ -743,18 +763,11 @@ __device__ __forceinline__ bool factor_forward(const GnArgs& a, const SmemLayout
     // ---- U(k)
     const int pw = (k + 1) % NW;  // panel wave of this step
     if (wave_o == pw) {
+      // the panel is the serial critical path of the factorization: issue it ahead
+      // of the co-resident waves (the other workgroup's and this one's MFMA work)
+      __builtin_amdgcn_s_setprio(3);
       double* DTn = DT + (k + 1) * DTS;
       if (k >= 0) {
-        // b_{k+1} -= U_{k,k+1}^T y_k (needed by the panel)
-        if (lane_o < 16) {
-          double s0 = 0.0, s1 = 0.0;
-#pragma unroll
-          for (int q = 0; q < 16; q += 2) {
-            s0 += PB[q * 16 + lane_o] * YV[16 * k + q];
-            s1 += PB[(q + 1) * 16 + lane_o] * YV[16 * k + q + 1];
-          }
-          BV[16 * (k + 1) + lane_o] -= s0 + s1;
-        }
         d4 t;
         double v[4];
 #pragma unroll
@@ -768,12 +781,12 @@ __device__ __forceinline__ bool factor_forward(const GnArgs& a, const SmemLayout
         for (int r = 0; r < 4; ++r) DTn[r * 64 + lane_o] = t[r];
         wave_lds_sync();
       }
-      wave_lds_sync();
-      if (!KO(3)) bad |= panel(DTn, BV + 16 * (k + 1), YV + 16 * (k + 1), lane_o);
+      if (!KO(3)) bad |= panel(DTn, lane_o);
+      __builtin_amdgcn_s_setprio(0);
     } else if (k >= 0 && !KO(4)) {
-      // b_b -= U_kb^T y_k for b >= k + 2: one output per lane of the other waves
+      // b_b -= U_kb^T y_k for b >= k + 1: one output per lane of the other waves
       const int vt = ((wave_o - pw - 1 + NW) % NW) * 64 + lane_o;
-      const int bq = k + 2 + (vt >> 4), c = vt & 15;
+      const int bq = k + 1 + (vt >> 4), c = vt & 15;
       if (bq < NT) {
         const double* ub = PB + (bq - k - 1) * 256 + c;
         double s0 = 0.0, s1 = 0.0;
@@ -848,6 +861,19 @@ __device__ __forceinline__ double rows4_sum(double v) {
          __longlong_as_double(((long long)h2[1] << 32) | (unsigned int)l2[1]);
 }
 
+__device__ __forceinline__ void block_fwd(const double* LT, const double* b, double* y, int lane) {
+  const int c = lane & 15, g = lane >> 4;
+  const double2 b01 = *(const double2*)(b + 4 * g);
+  const double2 b23 = *(const double2*)(b + 4 * g + 2);
+  const double* lt = LT + 4 * g * LIS + c;  // (L^-1)[c][s] = (L^-T)[s][c]
+  double s = lt[0] * b01.x;
+  s = fma(lt[LIS], b01.y, s);
+  s = fma(lt[2 * LIS], b23.x, s);
+  s = fma(lt[3 * LIS], b23.y, s);
+  const double yv = rows4_sum(s);
+  if (lane < 16) y[c] = yv;
+}
+
 // delta_k = L_kk^-T y_k, in place, by one whole wave: lane (c, g = l >> 4) sums
 // the four terms q = 4g..4g+3 of row c of L^-T, rows4_sum completes the dot.
 __device__ __forceinline__ void block_back(const double* LT, double* yv, int lane) {
@@ -875,7 +901,12 @@ __device__ __forceinline__ void backward(const GnArgs& a, const SmemLayout& SL, 
   const double* DT = sm + SL.DT;
   double* DV = sm + SL.YV;
   const int NT = a.NT;
-  if (wave == (NT - 1) % NW) block_back(DT + (NT - 1) * DTS, DV + 16 * (NT - 1), lane);
+  if (wave == (NT - 1) % NW) {
+    const double* BV = sm + SL.BV;
+    block_fwd(DT + (NT - 1) * DTS, BV + 16 * (NT - 1), DV + 16 * (NT - 1), lane);  // y_{NT-1}
+    wave_lds_sync();
+    block_back(DT + (NT - 1) * DTS, DV + 16 * (NT - 1), lane);
+  }
   __syncthreads();
 #pragma unroll 1
   for (int bb = NT - 1; bb >= 1 && !KO(5); --bb) {
@@ -897,8 +928,10 @@ __device__ __forceinline__ void backward(const GnArgs& a, const SmemLayout& SL, 
         for (int r = 0; r < 4; ++r)
           if ((lane_o & 15) == r) yj[(lane_o >> 4) + 4 * r] -= part[r];
         if (J == bb - 1) {
+          __builtin_amdgcn_s_setprio(3);
           wave_lds_sync();
           block_back(DT + J * DTS, yj, lane_o);
+          __builtin_amdgcn_s_setprio(0);
         }
       }
     }
@@ -909,7 +942,7 @@ __device__ __forceinline__ void backward(const GnArgs& a, const SmemLayout& SL, 
 #include "mhe_big.h"
 
 template <class DYN, class MEAS, int SLOTS, int mode, bool HUBER = false>
-__global__ __launch_bounds__(NTHREADS, 2) void k_gn(GnArgs a) {
+__global__ __launch_bounds__(NTHREADS, NW / 2) void k_gn(GnArgs a) {  // 2nd arg: min waves per SIMD (2 WGs per CU)
   constexpr int n = DYN::n;
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const ConstLayout CL = const_layout(a.P, a.M, n, MEAS::p, a.NT);

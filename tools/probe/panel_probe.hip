@@ -179,7 +179,7 @@ __global__ __launch_bounds__(64) void k_panel_probe(double* out, unsigned long l
     for (int t = lane; t < 256; t += 64) DT[t] = -A0[t];
     __syncthreads();
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-    if (V == 0) bad |= panel(DT, bk, yk, lane);
+    if (V == 0) bad |= panel(DT, lane);
     if (V == 1) bad |= panel_rawrsq(DT, bk, yk, lane);
     if (V == 2) bad |= panel_skel(DT, bk, yk, lane);
     if (V == 3) bad |= panel_dpp(DT, bk, yk, lane);
