@@ -157,16 +157,55 @@ __device__ __forceinline__ double readlane_d(double v, int lane) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
+// Butterfly step over lanes within a DPP row: quad_perm xor 1 / xor 2,
+// row_half_mirror, row_mirror -- each leaves every lane of the row holding the
+// combined value of its partner set.  Then v_permlane16/32_swap across rows.
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)b, CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// v_permlane16_swap (XOR16 = 1: row pairs) / v_permlane32_swap (2: wave halves)
+// with the same register as both operands leaves the two members of each pair in
+// [0] and [1] in every lane; OP combines them (sum / max).
+template <int XOR16, bool MAX>
+__device__ __forceinline__ double pair_combine(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = (int)b, hi = (int)(b >> 32);
+  double x, y;
+  if constexpr (XOR16 == 1) {
+    auto l = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    auto h = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    x = __longlong_as_double(((long long)h[0] << 32) | (unsigned int)l[0]);
+    y = __longlong_as_double(((long long)h[1] << 32) | (unsigned int)l[1]);
+  } else {
+    auto l = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    auto h = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    x = __longlong_as_double(((long long)h[0] << 32) | (unsigned int)l[0]);
+    y = __longlong_as_double(((long long)h[1] << 32) | (unsigned int)l[1]);
+  }
+  return MAX ? fmax(x, y) : x + y;
+}
+
 __device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
-  return v;
+  v += dpp_d<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_d<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_d<0x141>(v);  // row_half_mirror
+  v += dpp_d<0x140>(v);  // row_mirror
+  v = pair_combine<1, false>(v);
+  return pair_combine<2, false>(v);
 }
 
 __device__ __forceinline__ double wave_max(double v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v = fmax(v, __shfl_xor(v, o));
-  return v;
+  v = fmax(v, dpp_d<0xB1>(v));
+  v = fmax(v, dpp_d<0x4E>(v));
+  v = fmax(v, dpp_d<0x141>(v));
+  v = fmax(v, dpp_d<0x140>(v));
+  v = pair_combine<1, true>(v);
+  return pair_combine<2, true>(v);
 }
 
 // block-wide reduction of up to 2 values (sum or max), result broadcast
@@ -914,11 +953,15 @@ __device__ __forceinline__ void backward(const GnArgs& a, const SmemLayout& SL, 
     asm volatile("" : "+v"(lane_o));
     asm volatile("" : "+v"(stab_o));
     const double db = DV[16 * bb + (lane_o & 15)];
+    // slots in DESCENDING order: within row bb the tile (bb, bb-1) has the largest
+    // column-major index, and its owner's delta_{bb-1} is the critical chain
 #pragma unroll
-    for (int s = 0; s < SLOTS; ++s) {
+    for (int s = SLOTS - 1; s >= 0; --s) {
       const int IJ = slot_ij(stab_o, s);
       const int I = IJ & 0xffff, J = IJ >> 16;
-      if (IJ >= 0 && I == bb) {
+      if (IJ >= 0 && I == bb && (!KO(6) || J == bb - 1)) {
+        const bool crit = J == bb - 1;
+        if (crit) __builtin_amdgcn_s_setprio(3);
         double* yj = DV + 16 * J;
         double part[4];
 #pragma unroll
@@ -927,8 +970,7 @@ __device__ __forceinline__ void backward(const GnArgs& a, const SmemLayout& SL, 
 #pragma unroll
         for (int r = 0; r < 4; ++r)
           if ((lane_o & 15) == r) yj[(lane_o >> 4) + 4 * r] -= part[r];
-        if (J == bb - 1) {
-          __builtin_amdgcn_s_setprio(3);
+        if (crit) {
           wave_lds_sync();
           block_back(DT + J * DTS, yj, lane_o);
           __builtin_amdgcn_s_setprio(0);
