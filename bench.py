@@ -164,7 +164,7 @@ def main():
                        "parallelism": f"dp{world} (independent trajectories; RCCL broadcast of constants only)"},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None,
-                         "kernel": "mhe::k_gn<DynVanDerPol, MeasFullState<2>, 20, MODE_SOLVE>",
+                         "kernel": "mhe::k_gn<DynVanDerPol, MeasFullState<2>, 10, MODE_SOLVE, L2>",
                          "kernel_ms": kern_ms,
                          "flops_per_launch": fl,
                          "hbm_algorithmic_GBs": algorithmic_bytes_per_traj(w.P, w.n, w.m, w.M, w.p) * B / (kern_ms * 1e-3) / 1e9},
