@@ -227,6 +227,38 @@ int mhe_ekf_run(const mhe_ekf_dims* dims, int32_t batch, int32_t steps, double* 
                 const double* Q, const double* R, int64_t r_bstride, int64_t r_sstride,
                 double* mu_hist, double* S_hist, int32_t* status, void* stream);
 
+/* ------------------------------------------------------------------------
+ * Batched GNSS least-squares fixes (the MHE initialiser).
+ * Replaces utils/leastsquares.py:19-42 (iterativeLeastSquares),
+ * :45-63 (iterativeLeastSquaresVel) and the per-epoch loop of
+ * runLeastSquares (:97-141) for `chains` logs of `epochs` epochs each.
+ * ------------------------------------------------------------------------ */
+typedef struct mhe_ls_dims {
+  int32_t slots;     /* satellite slots per epoch in the arrays (<= 64) */
+  int32_t max_iter;  /* maxiter of iterativeLeastSquares (reference default 100); 0 = no position
+                        iterations (velocity at x_init: iterativeLeastSquaresVel alone) */
+  int32_t warm;      /* 1: epochs of a chain run in order, each starting from the previous fix
+                        (the reference's shared default x, utils/leastsquares.py:19,34);
+                        0: every epoch starts from x_init (all epochs in parallel) */
+  int32_t with_vel;  /* 1: also the velocity / bias-rate solve (utils/leastsquares.py:45-63) */
+  double tol;        /* stop when ||dx|| < tol (reference: 1e-7) */
+} mhe_ls_dims;
+
+/*
+ * Device pointers.  Per chain c and epoch k (e = c*epochs + k):
+ *   sat_pos (C,T,slots,3) ECEF, pr (C,T,slots), nsat (C,T): rows 0..nsat-1 valid
+ *   sat_vel (C,T,slots,3), pr_rate (C,T,slots): only with with_vel
+ *   x_init (C,3): starting position (b starts at 0 every epoch, as the reference)
+ * Outputs: x_out (C,T,3), b_out (C,T), v_out (C,T,3) / bd_out (C,T) with with_vel,
+ * iters_out (C,T) GN steps taken (-1: fewer than 4 independent satellites),
+ * x_last (C,3, optional, warm only) the chain's final position (the value the
+ * reference's shared default holds afterwards).  Returns MHE_OK or MHE_ERR_*.
+ */
+int mhe_ls_run(const mhe_ls_dims* dims, int32_t chains, int32_t epochs, const double* sat_pos,
+               const double* pr, const int32_t* nsat, const double* sat_vel, const double* pr_rate,
+               const double* x_init, double* x_out, double* b_out, double* v_out, double* bd_out,
+               int32_t* iters_out, double* x_last, void* stream);
+
 /* Library version string. */
 const char* mhe_version(void);
 

@@ -34,8 +34,13 @@ class MheEkfDims(ctypes.Structure):
                 ("dyn_model", c_i32), ("meas_model", c_i32), ("dt", c_dbl)]
 
 
+class MheLsDims(ctypes.Structure):
+    _fields_ = [("slots", c_i32), ("max_iter", c_i32), ("warm", c_i32), ("with_vel", c_i32), ("tol", c_dbl)]
+
+
 _P = ctypes.POINTER(MheDims)
 _PE = ctypes.POINTER(MheEkfDims)
+_PL = ctypes.POINTER(MheLsDims)
 SIGNATURES = {
     "mhe_version": (ctypes.c_char_p, []),
     "mhe_padded_dim": (c_i32, [_P]),
@@ -51,6 +56,8 @@ SIGNATURES = {
     "mhe_chol_solve": (ctypes.c_int, [_P, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "mhe_ekf_run": (ctypes.c_int, [_PE, c_i32, c_i32, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64,
                                    c_vp, c_i64, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "mhe_ls_run": (ctypes.c_int, [_PL, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                  c_vp, c_vp, c_vp, c_vp]),
 }
 
 

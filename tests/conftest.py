@@ -20,4 +20,4 @@ def pytest_configure(config):
 def golden():
     import numpy as np
     return {name: np.load(os.path.join(GOLDEN, name + ".npz"))
-            for name in ("collocation", "plugins", "ekf_gnss_stationary")}
+            for name in ("collocation", "plugins", "ekf_gnss_stationary", "least_squares")}

@@ -88,6 +88,9 @@ def load_reference():
         ref.gnss = _load("ref_gnss", f"{REF}/utils/gnss.py")
         ref.gutils = _load("ref_gutils", f"{REF}/utils/utils.py")
         ref.data = _load("ref_data", f"{REF}/utils/data.py")
+        sys.modules.setdefault("gnss", ref.gnss)     # leastsquares.py's flat imports
+        sys.modules.setdefault("utils", ref.gutils)
+        ref.ls = _load("ref_leastsquares", f"{REF}/utils/leastsquares.py")
     finally:
         sys.path.pop(0)
     return ref
@@ -319,12 +322,78 @@ def gen_gnss_io(ref):
     np.savez_compressed(os.path.join(OUT, "gnss_io.npz"), **out)
 
 
+def synth_constellation(rng, T, S, p0, vel, n_min=5):
+    """Seeded synthetic GNSS epochs (no reference data): satellites on a 26 560 km
+    shell above the receiver's horizon, receiver moving at ``vel`` (m/s) from
+    ``p0`` (ECEF), clock bias 3e4 m drifting 0.5 m/s; pseudoranges and rates with
+    1 m / 0.05 m/s noise.  Returns ragged per-epoch lists like load_gnss_logs."""
+    up = p0 / np.linalg.norm(p0)
+    sp, pr, sv, rr = [], [], [], []
+    for k in range(T):
+        pos = p0 + vel * k
+        b = 3e4 + 0.5 * k
+        c = int(rng.integers(n_min, S + 1))
+        dirs = rng.normal(size=(c, 3))
+        dirs /= np.linalg.norm(dirs, axis=1, keepdims=True)
+        dirs = np.where((dirs @ up)[:, None] < 0.2, -dirs, dirs)  # keep the upper hemisphere
+        dirs += 0.3 * up
+        dirs /= np.linalg.norm(dirs, axis=1, keepdims=True)
+        s = pos + 2.0e7 * dirs
+        s *= 26.56e6 / np.linalg.norm(s, axis=1, keepdims=True)
+        v = rng.normal(size=(c, 3)) * 2e3
+        los = (s - pos) / np.linalg.norm(s - pos, axis=1, keepdims=True)
+        sp.append(s)
+        sv.append(v)
+        pr.append(np.linalg.norm(s - pos, axis=1) + b + rng.normal(size=c))
+        rr.append(np.einsum("ij,ij->i", v - vel, los) + 0.5 + 0.05 * rng.normal(size=c))
+    return {"t": np.arange(T, dtype=np.float64), "sat_pos": sp, "pr": pr, "sat_vel": sv, "pr_rate": rr}
+
+
+def _pack_log(d, S=12):
+    """Ragged per-epoch lists -> fixed-slot arrays."""
+    T = len(d["pr"])
+    cnt = np.array([len(p) for p in d["pr"]], dtype=np.int32)
+    out = {"count": cnt, "t": np.asarray(d["t"], dtype=np.float64),
+           "sat_pos": np.zeros((T, S, 3)), "pr": np.zeros((T, S)),
+           "sat_vel": np.zeros((T, S, 3)), "pr_rate": np.zeros((T, S))}
+    for k in range(T):
+        c = cnt[k]
+        out["sat_pos"][k, :c] = d["sat_pos"][k]
+        out["pr"][k, :c] = d["pr"][k]
+        out["sat_vel"][k, :c] = d["sat_vel"][k]
+        out["pr_rate"][k, :c] = d["pr_rate"][k]
+    return out
+
+
+def gen_least_squares(ref):
+    """Reference runLeastSquares (utils/leastsquares.py:97-141) on two seeded
+    synthetic receivers run back to back in one process, as
+    gnss-multi-receiver.py:33-34 does -- the second log's first epoch warm-starts
+    from the first log's last fix through the shared default argument
+    (utils/leastsquares.py:19).  Inputs are synthetic; outputs are the
+    reference's."""
+    rng = np.random.default_rng(4242)
+    p_ref = ref.gutils.lla2ecef(np.array([37.4276, -122.1670, 0.0]))
+    out = {"p_ref": p_ref}
+    for tag, off, vel in (("A", [120.0, -40.0, 15.0], np.array([1.2, -0.7, 0.1])),
+                          ("B", [-300.0, 90.0, -20.0], np.array([-0.4, 0.9, 0.0]))):
+        d = synth_constellation(rng, 40, 12, p_ref + np.array(off), vel)
+        for k, v in _pack_log(d).items():
+            out[f"{tag}_{k}"] = v
+        sol = ref.ls.runLeastSquares(d["t"], d["sat_pos"], d["pr"], d["sat_vel"], d["pr_rate"], p_ref)
+        for key in ("x_ECEF", "y_ECEF", "z_ECEF", "bias", "xd_ECEF", "yd_ECEF", "zd_ECEF", "bias_rate",
+                    "x_ENU", "y_ENU", "z_ENU", "xd_ENU", "yd_ENU", "zd_ENU", "lat", "lon", "h"):
+            out[f"{tag}_ls_{key}"] = np.asarray(sol[key], dtype=np.float64)
+    np.savez_compressed(os.path.join(OUT, "least_squares.npz"), **out)
+
+
 def main():
     ref = load_reference()
     gen_collocation(ref)
     gen_plugins(ref)
     gen_ekf(ref)
     gen_gnss_io(ref)
+    gen_least_squares(ref)
     print("golden fixtures written to", OUT)
 
 
