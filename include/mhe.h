@@ -71,6 +71,33 @@ extern "C" {
 #define MHE_MEAS_PSEUDORANGE 2           /* :56-70 p=1, q=3 (sat_pos), idx[4] */
 #define MHE_MEAS_VEHICLE_PSEUDORANGE 3   /* :81-88 p=1, q=3               */
 #define MHE_MEAS_RANGE_3D 4              /* :39-54 p=1, q=3 ("y" form), idx[3] */
+#define MHE_MEAS_MIXED 5                 /* several scalar plug-ins in one problem (one
+                                            addResidualCost call each, nlp/nlp.py:258-277):
+                                            p=1, q=MHE_MIXED_Q, every row names its model */
+
+/* MHE_MEAS_MIXED rows: PAR row = [code, i0..i6, v0..v5] (q = 14).  Indices point
+ * into the augmented vector [x(t_i) (n) ; z (n_extra)] -- z are the extra decision
+ * variables (addVariables beyond the state, e.g. XA in multi-receiver.py:73,99);
+ * -1 = unused term.  h per code (reference nlp/measurements.py):
+ *   PSEUDORANGE       :56-70  |x[i0..i2] - v0..2| + x[i3]
+ *   PSEUDORANGE_RATE  :72-79  (v3..5 - x[i3..i5]) . (v0..2 - x[i0..i2]) / |.| + x[i6]
+ *   RANGE_2D          :7-20   sqrt(sum_k (x[i_k] - x[i_{k+2}] - v_k)^2 + 1e-6), k < 2
+ *   RANGE_3D          :39-54  sqrt(sum_k (x[i_k] - x[i_{k+3}] - v_k)^2 + 1e-6), k < 3
+ *                             (both forms: "idxA/idxB" -> i = A, B; "y" -> i = idx, -1
+ *                             and v = y, or with y a decision variable i = idx, n + j)
+ *   HEADING_2D        :22-37  atan2(x[i0] - x[i1] + v0, x[i2] - x[i3] + v1)
+ *   COMPONENT         :4-5    x[i0] (full_state as scalar rows)
+ *   NONE                      h = 0 (padding row; give it R = 0) */
+#define MHE_MIXED_Q 14
+#define MHE_ROW_NONE 0
+#define MHE_ROW_PSEUDORANGE 1
+#define MHE_ROW_PSEUDORANGE_RATE 2
+#define MHE_ROW_RANGE_2D 3
+#define MHE_ROW_RANGE_3D 4
+#define MHE_ROW_HEADING_2D 5
+#define MHE_ROW_COMPONENT 6
+#define MHE_MAX_EXTRA 4   /* extra decision variables per trajectory */
+#define MHE_MAX_EQ 48     /* n_extra + n_eq */
 
 typedef struct mhe_dims {
   int32_t N;            /* collocation order; P = N + 1 CGL nodes            */
@@ -90,6 +117,13 @@ typedef struct mhe_dims {
   int32_t bound_idx[8]; /* bounded component indices (< n)                   */
   double bound_lb[8];   /* lower / upper bounds (+-inf allowed), every node  */
   double bound_ub[8];
+  int32_t n_extra;      /* extra decision variables z (<= MHE_MAX_EXTRA); they
+                           enter MHE_MEAS_MIXED rows only                        */
+  int32_t n_eq;         /* addEqConstraint(equality_constaint, [a, b]) rows
+                           (nlp/nlp.py:52-53, nlp/constraints.py): v[a] - v[b] = 0 */
+  const int32_t* eq_idx;/* HOST pointer, 2*n_eq entries (a, b) into the flattened
+                           state vector v = X (P*n, node-major: j*n + c); b = -1
+                           means v[a] = 0.  Copied into the constants buffer.     */
 } mhe_dims;
 
 /* Dynamics cost (addDynamicsCost, nlp/nlp.py:242-245): */
@@ -97,7 +131,16 @@ typedef struct mhe_dims {
 #define MHE_COST_HUBER 1  /* cost_functions.pseudo_huber_loss (cost_functions.py:25-31): IRLS
                              weights q_a / sqrt(1 + W_a^2 / delta^2), only diag(Qw) enters */
 /* Bounds (addVarBounds, nlp/nlp.py:314-317) are enforced by projecting every GN
- * step onto the box (projected Gauss-Newton). */
+ * step onto the box (projected Gauss-Newton).
+ * Extra variables and equality constraints run on the
+ * large-system path: each GN step solves the bordered (KKT) system
+ *   [ H    H_xz  C^T ] [dx]   [-g  ]
+ *   [ H_zx H_zz  0   ] [dz] = [-g_z]
+ *   [ C    0     0   ] [l ]   [-c  ]
+ * through the Cholesky factor of H (one multi-RHS solve of the border columns,
+ * a small quasi-definite LDL^T of the Schur complement).  Linear constraints are
+ * therefore met exactly after every step.  Bounds and constraints together are
+ * not supported (MHE_ERR_UNSUPPORTED). */
 
 /* Size in bytes of the device constants buffer for `dims` (0 on bad dims). */
 size_t mhe_const_bytes(const mhe_dims* dims);
@@ -167,6 +210,22 @@ int mhe_gn_solve_ws(const mhe_dims* dims, const void* const_buf, int32_t batch,
                     double* cost_out, int32_t* iters_out, int32_t* status_out,
                     int32_t max_iter, double tol, void* workspace, size_t workspace_bytes,
                     void* stream);
+
+/*
+ * mhe_gn_solve_ws with extra decision variables: Z0 / Z_out (B, n_extra) device
+ * arrays (initial values / solution; NULL when n_extra == 0).  Problems with
+ * n_extra > 0, n_eq > 0 or MHE_MEAS_MIXED always take the large-system path
+ * (workspace required).  The stopping rule covers z too:
+ * max|(dx, dz)| <= tol * (1 + max|(X, z)|).
+ */
+int mhe_gn_solve_ext(const mhe_dims* dims, const void* const_buf, int32_t batch,
+                     const double* X0, double* X_out, const double* Z0, double* Z_out,
+                     const double* U, int64_t u_bstride,
+                     const double* Y, const double* PAR, int64_t par_bstride,
+                     const double* x0,
+                     double* cost_out, int32_t* iters_out, int32_t* status_out,
+                     int32_t max_iter, double tol, void* workspace, size_t workspace_bytes,
+                     void* stream);
 
 /*
  * Kernel-level parity: assemble the GN normal equations at X.

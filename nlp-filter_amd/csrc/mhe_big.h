@@ -17,7 +17,12 @@
 //                  (diagonal blocks through the same single-wave panel as k_gn,
 //                  MFMA TRSM and trailing updates, block column cached in LDS
 //                  when it fits) + forward and backward solves
-//   k_big_update   X += delta (back to node-major), convergence / status
+//   k_big_border   (extra variables z / equality constraints)
+//                  bordered KKT step through the factor: H Z = [H_xz C^T] by a
+//                  16-column MFMA forward/backward substitution, Schur complement
+//                  S - B^T Z, LDL^T (quasi-definite: z pivots > 0, constraint
+//                  pivots < 0), delta -= Z w
+//   k_big_update   X += delta (back to node-major), z += dz, convergence / status
 // Converged or failed trajectories are frozen by a per-trajectory state word,
 // so the host loop only enqueues (no synchronisation).
 
@@ -28,10 +33,10 @@ constexpr int BIG_RUNNING = -1;
 __host__ __device__ inline int big_pp(int P) { return 16 * ((P + 15) / 16); }
 
 struct BigConst {  // byte offsets into the constants buffer
-  size_t D, Dt, DCD, cw, Qw, Pw, Rw, PhiE, PhiET, erow, ne, flag, total;
+  size_t D, Dt, DCD, cw, Qw, Pw, Rw, PhiE, PhiET, erow, ne, flag, eq, total;
 };
 
-__host__ __device__ inline BigConst big_const_layout(int P, int M, int n, int p) {
+__host__ __device__ inline BigConst big_const_layout(int P, int M, int n, int p, int nc = 0) {
   BigConst L;
   size_t o = 0;
   const int Mr = M > 0 ? M : 1;
@@ -47,15 +52,17 @@ __host__ __device__ inline BigConst big_const_layout(int P, int M, int n, int p)
   L.erow = o;  o = align256(o + sizeof(int) * (Mr + 1));    // first row of each epoch, erow[E] = M
   L.ne = o;    o = align256(o + sizeof(int));               // E
   L.flag = o;  o = align256(o + sizeof(int) * Mr);          // scratch: row starts a new epoch
+  L.eq = o;    o = align256(o + sizeof(int) * 2 * (nc > 0 ? nc : 1));  // equality-constraint index pairs
   L.total = o;
   return L;
 }
 
 struct BigWs {  // per-trajectory workspace offsets in doubles
-  size_t H, LT, BV, YV, XE, GEe, Ge, Es, FtE, Vs, FtV, total;
+  size_t H, LT, BV, YV, XE, GEe, Ge, Es, FtE, Vs, FtV, GZe, HZZe, GZVe, BM, ZM, DZ, total;
 };
 
-__host__ __device__ inline BigWs big_ws_layout(int P, int M, int n, int NT) {
+// nz extra variables, nc equality constraints (border of the KKT system)
+__host__ __device__ inline BigWs big_ws_layout(int P, int M, int n, int NT, int nz = 0, int nc = 0) {
   BigWs W;
   size_t o = 0;
   const size_t ntiles = (size_t)NT * (NT + 1) / 2;
@@ -73,6 +80,13 @@ __host__ __device__ inline BigWs big_ws_layout(int P, int M, int n, int NT) {
   W.FtE = o; o = al(o + (size_t)P * n * n);
   W.Vs = o;  o = al(o + (size_t)P * n);
   W.FtV = o; o = al(o + (size_t)P * n);
+  const int NZX = nz > 0 ? MHE_MAX_EXTRA : 0, K = nz + nc;
+  W.GZe = o;  o = al(o + (size_t)(nz > 0 ? Mr : 0) * n * NZX);   // per epoch  sum H_x^T R H_z
+  W.HZZe = o; o = al(o + (size_t)(nz > 0 ? Mr : 0) * NZX * NZX); //            sum H_z^T R H_z
+  W.GZVe = o; o = al(o + (size_t)(nz > 0 ? Mr : 0) * NZX);       //            sum H_z^T R e
+  W.BM = o;   o = al(o + (size_t)K * dp);                        // border columns [H_xz C^T]
+  W.ZM = o;   o = al(o + (size_t)((K + 15) / 16) * 16 * dp);     // H^-1 [H_xz C^T] (16-col panels)
+  W.DZ = o;   o = al(o + (size_t)NZX);                           // z step
   W.total = o;
   return W;
 }
@@ -99,6 +113,8 @@ struct BigArgs {
   int n_bounds;      // projected GN (addVarBounds)
   int bidx[8];
   double blb[8], bub[8];
+  int nz, nc;        // extra variables / equality constraints (f4)
+  double* Z;         // (B, nz) current extra variables (Z_out)
 };
 
 __device__ __forceinline__ int big_tile_index(int I, int J, int NT) { return J * NT - J * (J - 1) / 2 + (I - J); }
@@ -109,8 +125,8 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_resid(BigArgs a, int final
   constexpr int n = DYN::n, m = DYN::m, p = MEAS::p, q = MEAS::q;
   const int b = blockIdx.x;
   if (!final_pass && a.state[b] != BIG_RUNNING) return;
-  const BigConst CL = big_const_layout(a.P, a.M, n, p);
-  const BigWs WL = big_ws_layout(a.P, a.M, n, a.NT);
+  const BigConst CL = big_const_layout(a.P, a.M, n, p, a.nc);
+  const BigWs WL = big_ws_layout(a.P, a.M, n, a.NT, a.nz, a.nc);
   double* ws = a.ws + (size_t)b * a.ws_stride;
   const double* D = (const double*)(a.cbuf + CL.D);
   const double* Dt = (const double*)(a.cbuf + CL.Dt);
@@ -183,6 +199,51 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_resid(BigArgs a, int final
   }
   __syncthreads();
   // measurement rows grouped by epoch (nlp/nlp.py:264-273)
+  if constexpr (MEAS::MIXED) {
+    // scalar rows of several plug-ins over [x(t_e) ; z]; the z couplings are
+    // accumulated per epoch for k_big_border
+    constexpr int NA = MEAS::NA, NZX = MHE_MAX_EXTRA;
+    const int nz = a.nz;
+    for (int e = threadIdx.x; e < E; e += BIG_NTHREADS) {
+      double xt[NA], ge[n], G[n * n], Gz[n * NZX], Hzz[NZX * NZX], gz[NZX];
+      for (int c = 0; c < n; ++c) {
+        xt[c] = ws[WL.XE + e * n + c];
+        ge[c] = 0.0;
+      }
+      for (int c = 0; c < NZX; ++c) {
+        xt[n + c] = c < nz ? a.Z[(size_t)b * nz + c] : 0.0;
+        gz[c] = 0.0;
+      }
+      for (int c = 0; c < n * n; ++c) G[c] = 0.0;
+      for (int c = 0; c < n * NZX; ++c) Gz[c] = 0.0;
+      for (int c = 0; c < NZX * NZX; ++c) Hzz[c] = 0.0;
+      for (int i = erow[e]; i < erow[e + 1]; ++i) {
+        const double* PR = a.PAR + (long long)b * a.pstride + (long long)i * q;
+        double h, Gr[NA];
+        MEAS::eval(xt, PR, nz, h, Gr);
+        const double R = Rw[i];
+        const double ev = a.Y[(long long)b * a.M + i] - h, Re = R * ev;
+        cost += ev * Re;
+        for (int c = 0; c < n; ++c) {
+          ge[c] += Gr[c] * Re;
+          const double rc = R * Gr[c];
+          for (int r = 0; r < n; ++r) G[r * n + c] += Gr[r] * rc;
+          for (int z = 0; z < nz; ++z) Gz[c * NZX + z] += rc * Gr[n + z];
+        }
+        for (int z = 0; z < nz; ++z) {
+          gz[z] += Gr[n + z] * Re;
+          for (int z2 = 0; z2 < nz; ++z2) Hzz[z * NZX + z2] += Gr[n + z] * R * Gr[n + z2];
+        }
+      }
+      for (int c = 0; c < n; ++c) ws[WL.GEe + e * n + c] = ge[c];
+      for (int c = 0; c < n * n; ++c) ws[WL.Ge + e * n * n + c] = G[c];
+      if (nz > 0) {
+        for (int c = 0; c < n * NZX; ++c) ws[WL.GZe + (size_t)e * n * NZX + c] = Gz[c];
+        for (int c = 0; c < NZX * NZX; ++c) ws[WL.HZZe + (size_t)e * NZX * NZX + c] = Hzz[c];
+        for (int c = 0; c < NZX; ++c) ws[WL.GZVe + (size_t)e * NZX + c] = gz[c];
+      }
+    }
+  } else
   for (int e = threadIdx.x; e < E; e += BIG_NTHREADS) {
     double xe[n], ge[n], G[n * n];
     for (int c = 0; c < n; ++c) {
@@ -271,8 +332,8 @@ __global__ __launch_bounds__(256) void k_big_assemble(BigArgs a) {
   constexpr int n = DYN::n, p = MEAS::p;
   const int b = blockIdx.y;
   if (a.state[b] != BIG_RUNNING) return;
-  const BigConst CL = big_const_layout(a.P, a.M, n, p);
-  const BigWs WL = big_ws_layout(a.P, a.M, n, a.NT);
+  const BigConst CL = big_const_layout(a.P, a.M, n, p, a.nc);
+  const BigWs WL = big_ws_layout(a.P, a.M, n, a.NT, a.nz, a.nc);
   const double* ws = a.ws + (size_t)b * a.ws_stride;
   double* H = a.ws + (size_t)b * a.ws_stride + WL.H;
   const double* D = (const double*)(a.cbuf + CL.D);
@@ -330,7 +391,7 @@ __global__ __launch_bounds__(256) void k_big_assemble(BigArgs a) {
 __global__ __launch_bounds__(BIG_NTHREADS) void k_big_chol(BigArgs a) {
   const int b = blockIdx.x;
   if (a.state[b] != BIG_RUNNING) return;
-  const BigWs WL = big_ws_layout(a.P, a.M, a.n, a.NT);
+  const BigWs WL = big_ws_layout(a.P, a.M, a.n, a.NT, a.nz, a.nc);
   double* ws = a.ws + (size_t)b * a.ws_stride;
   double* H = ws + WL.H;
   double* LTg = ws + WL.LT;
@@ -449,17 +510,221 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_chol(BigArgs a) {
   }
 }
 
+// ------------------------------------------------------------ border (f4)
+// Bordered Gauss-Newton step for extra variables z and equality constraints
+// C v = 0 (include/mhe.h).  Runs after k_big_chol, which left the factor
+// H = L L^T (L_Ik tiles in place, L_kk^-T in LT) and the unconstrained step
+// du = -H^-1 g in YV.  With B = [H_xz  C^T] (dp x K), S = [H_zz 0; 0 0]:
+//   Z = H^-1 B                 (16-column panels: MFMA forward/backward substitution)
+//   (S - B^T Z) w = r - B^T du,  r = [-g_z ; -c(v)]
+//   dx = du - Z w,  dz = w[0:nz]
+// The Schur matrix is quasi-definite (z block SPD, constraint block negative
+// definite), so LDL^T without pivoting is stable; a z component no row depends on
+// (zero pivot with a zero row) is held fixed (dz = 0), the minimum-norm choice.
+// Dynamic LDS: K*K (Schur) + 2K (rhs / w, pivot column) doubles.
+template <int n>
+__global__ __launch_bounds__(BIG_NTHREADS) void k_big_border(BigArgs a) {
+  constexpr int NZX = MHE_MAX_EXTRA;
+  const int b = blockIdx.x;
+  if (a.state[b] != BIG_RUNNING) return;
+  const BigConst CL = big_const_layout(a.P, a.M, n, 1, a.nc);
+  const BigWs WL = big_ws_layout(a.P, a.M, n, a.NT, a.nz, a.nc);
+  double* ws = a.ws + (size_t)b * a.ws_stride;
+  const double* H = ws + WL.H;
+  const double* LT = ws + WL.LT;
+  double* YV = ws + WL.YV;
+  double* BM = ws + WL.BM;
+  double* ZM = ws + WL.ZM;
+  const double* PhiE = (const double*)(a.cbuf + CL.PhiE);
+  const int* eq = (const int*)(a.cbuf + CL.eq);
+  const int E = a.M > 0 ? *(const int*)(a.cbuf + CL.ne) : 0;
+  const int nz = a.nz, nc = a.nc, K = nz + nc, KP = (K + 15) / 16 * 16;
+  const int NT = a.NT, Pp = a.Pp, dp = 16 * NT;
+  const double* X = a.X + (size_t)b * a.P * n;
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  double* Ms = sm;            // K x K Schur complement, then its LDL^T
+  double* rw = sm + K * K;    // K: right-hand side, then w
+  double* lc = rw + K;        // K: pivot column of the current LDL^T step
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+
+  // (1) border columns, component-major rows r = c*Pp + j (padding rows 0);
+  //     ZM columns K..KP-1 are zero (inert panel columns)
+  for (int t = threadIdx.x; t < KP * dp; t += BIG_NTHREADS) {
+    const int col = t / dp, r = t % dp, ca = r / Pp, j = r % Pp;
+    double v = 0.0;
+    if (col < K && j < a.P) {
+      if (col < nz) {
+        for (int e = 0; e < E; ++e) v += PhiE[(size_t)e * a.P + j] * ws[WL.GZe + ((size_t)e * n + ca) * NZX + col];
+      } else {
+        const int fi = j * n + ca;  // node-major index of this row
+        if (eq[2 * (col - nz)] == fi) v += 1.0;
+        if (eq[2 * (col - nz) + 1] == fi) v -= 1.0;
+      }
+    }
+    if (col < K) BM[(size_t)col * dp + r] = v;
+    ZM[(size_t)col * dp + r] = v;
+  }
+  __syncthreads();
+
+  // (2) Z = H^-1 B in place in ZM, one 16-column panel at a time.  MFMA operand
+  //     layout as in k_big_chol: A[i = l&15][m = 4r + (l>>4)], B[m][j = l&15],
+  //     C[(l>>4) + 4r][l&15].  ZM is column-major (col*dp + row).
+  const int ii = lane & 15, mg = lane >> 4;
+  for (int p0 = 0; p0 < K; p0 += 16) {
+    double* Zp = ZM + (size_t)p0 * dp;
+    auto zload = [&](int blk, int r) { return Zp[(size_t)ii * dp + 16 * blk + 4 * r + mg]; };       // B[m][j]
+    for (int k = 0; k < NT; ++k) {  // forward: Y_k = L_kk^-1 Z_k;  Z_I -= L_Ik Y_k
+      if (wave == 0) {
+        d4 c = {0.0, 0.0, 0.0, 0.0};
+        double av[4], bv[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          av[r] = LT[(size_t)k * DTS + (4 * r + mg) * LIS + ii];  // (L^-1)[i][m] = (L^-T)[m][i]
+          bv[r] = zload(k, r);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) c = __builtin_amdgcn_mfma_f64_16x16x4f64(av[r], bv[r], c, 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Zp[(size_t)ii * dp + 16 * k + mg + 4 * r] = c[r];
+      }
+      __syncthreads();
+      for (int I = k + 1 + wave; I < NT; I += BIG_NW) {
+        const double* L = H + (size_t)big_tile_index(I, k, NT) * 256;
+        d4 c;
+        double av[4], bv[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          c[r] = Zp[(size_t)ii * dp + 16 * I + mg + 4 * r];
+          av[r] = -L[ii * 16 + 4 * r + mg];
+          bv[r] = zload(k, r);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) c = __builtin_amdgcn_mfma_f64_16x16x4f64(av[r], bv[r], c, 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Zp[(size_t)ii * dp + 16 * I + mg + 4 * r] = c[r];
+      }
+      __syncthreads();
+    }
+    for (int k = NT - 1; k >= 0; --k) {  // backward: Z_k = L_kk^-T Y_k;  Y_J -= L_kJ^T Z_k
+      if (wave == 0) {
+        d4 c = {0.0, 0.0, 0.0, 0.0};
+        double av[4], bv[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          av[r] = LT[(size_t)k * DTS + ii * LIS + 4 * r + mg];  // (L^-T)[i][m]
+          bv[r] = zload(k, r);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) c = __builtin_amdgcn_mfma_f64_16x16x4f64(av[r], bv[r], c, 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Zp[(size_t)ii * dp + 16 * k + mg + 4 * r] = c[r];
+      }
+      __syncthreads();
+      for (int J = wave; J < k; J += BIG_NW) {
+        const double* L = H + (size_t)big_tile_index(k, J, NT) * 256;
+        d4 c;
+        double av[4], bv[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          c[r] = Zp[(size_t)ii * dp + 16 * J + mg + 4 * r];
+          av[r] = -L[(4 * r + mg) * 16 + ii];  // (L_kJ^T)[i][m] = L_kJ[m][i]
+          bv[r] = zload(k, r);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) c = __builtin_amdgcn_mfma_f64_16x16x4f64(av[r], bv[r], c, 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Zp[(size_t)ii * dp + 16 * J + mg + 4 * r] = c[r];
+      }
+      __syncthreads();
+    }
+  }
+
+  // (3) Schur complement and right-hand side (one wave per entry, lanes over rows)
+  for (int t = wave; t < K * K + K; t += BIG_NW) {
+    const bool isr = t >= K * K;
+    const int r = isr ? t - K * K : t / K, c = isr ? 0 : t % K;
+    const double* x = BM + (size_t)r * dp;
+    const double* y = isr ? YV : ZM + (size_t)c * dp;
+    double s = 0.0;
+    for (int i = lane; i < dp; i += 64) s += x[i] * y[i];
+    s = wave_sum(s);
+    if (lane == 0) {
+      if (isr) {
+        double base;
+        if (r < nz) {  // -g_z = sum H_z^T R e
+          base = 0.0;
+          for (int e = 0; e < E; ++e) base += ws[WL.GZVe + (size_t)e * NZX + r];
+        } else {       // -c(v)
+          const int ia = eq[2 * (r - nz)], ib = eq[2 * (r - nz) + 1];
+          base = -(X[ia] - (ib >= 0 ? X[ib] : 0.0));
+        }
+        rw[r] = base - s;
+      } else {
+        double sv = 0.0;
+        if (r < nz && c < nz)
+          for (int e = 0; e < E; ++e) sv += ws[WL.HZZe + (size_t)e * NZX * NZX + r * NZX + c];
+        Ms[r * K + c] = sv - s;
+      }
+    }
+  }
+  __syncthreads();
+
+  // (4) LDL^T (right-looking, lanes over rows) and the solve, wave 0
+  if (wave == 0) {
+    // lower triangle only; the pivot column is snapshotted into lc before the
+    // rank-1 update so no lane reads an entry another lane has already scaled
+    for (int j = 0; j < K; ++j) {
+      const double d = Ms[j * K + j];
+      // exactly zero pivot: an extra variable no residual depends on (its row and
+      // column are exactly zero) -- held fixed.  A NaN pivot propagates into the
+      // step and the trajectory fails the finiteness test in k_big_update.
+      const bool skip = d == 0.0;
+      for (int i = j + 1 + lane; i < K; i += 64) lc[i] = Ms[i * K + j];
+      wave_lds_sync();
+      for (int i = j + 1 + lane; i < K; i += 64) {
+        const double l = skip ? 0.0 : lc[i] / d;
+        for (int c = j + 1; c <= i; ++c) Ms[i * K + c] -= l * lc[c];
+        Ms[i * K + j] = l;  // unit-lower L below the diagonal
+      }
+      if (lane == 0 && skip) Ms[j * K + j] = 0.0;  // D_j = 0 marks a held variable
+      wave_lds_sync();
+    }
+    if (lane == 0) {
+      for (int i = 0; i < K; ++i)  // L y = r
+        for (int c = 0; c < i; ++c) rw[i] -= Ms[i * K + c] * rw[c];
+      for (int i = 0; i < K; ++i) rw[i] = Ms[i * K + i] != 0.0 ? rw[i] / Ms[i * K + i] : 0.0;
+      for (int i = K - 1; i >= 0; --i)  // L^T w = y
+        for (int c = i + 1; c < K; ++c) rw[i] -= Ms[c * K + i] * rw[c];
+    }
+  }
+  __syncthreads();
+
+  // (5) dx = du - Z w,  dz = w[0:nz]
+  for (int i = threadIdx.x; i < dp; i += BIG_NTHREADS) {
+    double s = YV[i];
+    for (int c = 0; c < K; ++c) s -= ZM[(size_t)c * dp + i] * rw[c];
+    YV[i] = s;
+  }
+  if (threadIdx.x < NZX) ws[WL.DZ + threadIdx.x] = threadIdx.x < nz ? rw[threadIdx.x] : 0.0;
+}
+
 // ------------------------------------------------------------ update
 template <int n>
 __global__ __launch_bounds__(256) void k_big_update(BigArgs a) {
   const int b = blockIdx.x;
   if (a.state[b] != BIG_RUNNING) return;
-  const BigWs WL = big_ws_layout(a.P, a.M, n, a.NT);
+  const BigWs WL = big_ws_layout(a.P, a.M, n, a.NT, a.nz, a.nc);
   const double* YV = a.ws + (size_t)b * a.ws_stride + WL.YV;
   double* X = a.X + (size_t)b * a.P * n;
   __shared__ double red[8];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   double dmax = 0.0, fin = 0.0;
+  const double* DZ = a.ws + (size_t)b * a.ws_stride + WL.DZ;
+  if (threadIdx.x < a.nz) {  // extra variables (f4): same stopping rule
+    const double dv = DZ[threadIdx.x];
+    if (!isfinite(dv)) fin = 1.0;
+    dmax = fabs(dv);
+  }
   for (int t = threadIdx.x; t < a.P * n; t += 256) {
     const int j = t / n, c = t % n;
     const double dv = YV[c * a.Pp + j];
@@ -487,6 +752,11 @@ __global__ __launch_bounds__(256) void k_big_update(BigArgs a) {
     return;
   }
   double xmax = 0.0;
+  if (threadIdx.x < a.nz) {
+    double* zp = a.Z + (size_t)b * a.nz + threadIdx.x;
+    *zp += DZ[threadIdx.x];
+    xmax = fabs(*zp);
+  }
   for (int t = threadIdx.x; t < a.P * n; t += 256) {
     const int j = t / n, c = t % n;
     double xv = X[t] + YV[c * a.Pp + j];
@@ -541,6 +811,17 @@ __global__ void k_big_consts(int P, int M, int n, int p, const double* D, const 
     ((double*)(cbuf + CL.Pw))[e] = Pw ? Pw[e] : 0.0;
   }
   for (int e = gid; e < M * p * p; e += stride) ((double*)(cbuf + CL.Rw))[e] = Rw[e];
+}
+
+// equality-constraint index pairs, passed by value (kernel arguments) so that
+// building constants stays a pure stream-ordered enqueue
+struct EqPairs {
+  int v[2 * MHE_MAX_EQ];
+};
+__global__ void k_big_eq_consts(int P, int M, int n, int p, int nc, EqPairs e, char* cbuf) {
+  const BigConst CL = big_const_layout(P, M, n, p, nc);
+  int* o = (int*)(cbuf + CL.eq);
+  for (int i = threadIdx.x; i < 2 * nc; i += blockDim.x) o[i] = e.v[i];
 }
 
 // epoch detection: row i starts an epoch unless its Phi row equals row i-1 bitwise

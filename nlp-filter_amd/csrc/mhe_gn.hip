@@ -1248,6 +1248,7 @@ bool meas_info(int id, int n, int& p, int& q, bool& linear) {
     case MHE_MEAS_PSEUDORANGE: p = 1; q = 3; linear = false; return true;
     case MHE_MEAS_VEHICLE_PSEUDORANGE: p = 1; q = 3; linear = false; return true;
     case MHE_MEAS_RANGE_3D: p = 1; q = 3; linear = false; return true;
+    case MHE_MEAS_MIXED: p = 1; q = MHE_MIXED_Q; linear = false; return true;
   }
   return false;
 }
@@ -1255,9 +1256,12 @@ bool meas_info(int id, int n, int& p, int& q, bool& linear) {
 // Register-resident path iff the node-major padded system fits MAX_NT tiles.
 // MHE_FORCE_BIG=1 (tests only) routes every problem through the large-system
 // path so both paths can be compared on identical inputs.
+// Mixed-row problems, extra variables and equality constraints
+// always take the large-system path (it carries the bordered KKT step).
 bool is_big(const mhe_dims* dm) {
   const char* f = getenv("MHE_FORCE_BIG");
   if (f && f[0] == '1') return true;
+  if (dm->meas_model == MHE_MEAS_MIXED || dm->n_extra > 0 || dm->n_eq > 0) return true;
   return ((dm->N + 1) * dm->n + 15) / 16 > MAX_NT;
 }
 
@@ -1280,6 +1284,17 @@ int check_dims(const mhe_dims* dm, int* NT_out) {
         (dm->meas_model == MHE_MEAS_RANGE_3D && i < 3 && (dm->meas_idx[i] < 0 || dm->meas_idx[i] >= n)))
       return MHE_ERR_DIMS;
   const int P = dm->N + 1;
+  if (dm->n_extra < 0 || dm->n_extra > MHE_MAX_EXTRA || dm->n_eq < 0 || dm->n_extra + dm->n_eq > MHE_MAX_EQ)
+    return MHE_ERR_DIMS;
+  if (dm->n_extra > 0 && dm->meas_model != MHE_MEAS_MIXED) return MHE_ERR_DIMS;  // z enters mixed rows only
+  if (dm->n_eq > 0) {
+    if (!dm->eq_idx) return MHE_ERR_NULL;
+    for (int i = 0; i < dm->n_eq; ++i) {
+      const int ia = dm->eq_idx[2 * i], ib = dm->eq_idx[2 * i + 1];
+      if (ia < 0 || ia >= P * n || ib < -1 || ib >= P * n || ia == ib) return MHE_ERR_DIMS;
+    }
+  }
+  if (dm->n_bounds > 0 && (dm->n_eq > 0 || dm->n_extra > 0)) return MHE_ERR_UNSUPPORTED;
   int NT = (P * n + 15) / 16;
   if (is_big(dm)) NT = n * big_pp(P) / 16;  // large-system path (mhe_big.h), component-major tiles
   if (NT_out) *NT_out = NT;
@@ -1295,6 +1310,9 @@ int smem_bytes(const mhe_dims* dm, int NT) {
 
 template <class DYN, class MEAS>
 int launch_gn(const mhe_dims* dm, GnArgs& a, int batch, int mode, hipStream_t st) {
+  if constexpr (MEAS::MIXED) {
+    return MHE_ERR_UNSUPPORTED;  // mixed rows: large-system path only
+  } else {
   int smem = smem_bytes(dm, a.NT);
   if (const char* pad = getenv("MHE_DEBUG_SMEM_PAD")) smem += atoi(pad);  // debug: force occupancy
   if (smem > 160 * 1024) return MHE_ERR_UNSUPPORTED;
@@ -1308,6 +1326,7 @@ int launch_gn(const mhe_dims* dm, GnArgs& a, int batch, int mode, hipStream_t st
     return MHE_ERR_HIP;
   hipLaunchKernelGGL(kern, dim3(batch), dim3(NTHREADS), smem, st, a);
   return hipGetLastError() == hipSuccess ? MHE_OK : MHE_ERR_HIP;
+  }
 }
 
 template <class MEAS>
@@ -1322,8 +1341,16 @@ int launch_cc(const mhe_dims* dm, int NT, const double* D, const double* cw, con
       hipLaunchKernelGGL(k_big_epoch_scan, dim3(1), dim3(1), 0, st, P, dm->M, dm->n, dm->p, cbuf);
       hipLaunchKernelGGL(k_big_epoch_rows, dim3(256), dim3(256), 0, st, P, dm->M, dm->n, dm->p, Phi, cbuf);
     }
+    if (dm->n_eq > 0) {
+      EqPairs e = {};
+      for (int i = 0; i < 2 * dm->n_eq; ++i) e.v[i] = dm->eq_idx[i];
+      hipLaunchKernelGGL(k_big_eq_consts, dim3(1), dim3(128), 0, st, P, dm->M, dm->n, dm->p, dm->n_eq, e, cbuf);
+    }
     return hipGetLastError() == hipSuccess ? MHE_OK : MHE_ERR_HIP;
   }
+  if constexpr (MEAS::MIXED) {
+    return MHE_ERR_UNSUPPORTED;
+  } else {
   const int ntiles = NT * (NT + 1) / 2;
   hipLaunchKernelGGL(k_copy_consts, dim3(256), dim3(256), 0, st, P, dm->M, dm->n, dm->p, NT, D, cw, Phi, Qw,
                      Rw, Pw, cbuf);
@@ -1331,6 +1358,7 @@ int launch_cc(const mhe_dims* dm, int NT, const double* D, const double* cw, con
                      dm->p, NT, dm->has_prior, dm->dyn_cost == MHE_COST_HUBER ? 1 : 0, 2.0 / dm->T, D, cw, Phi,
                      Qw, Rw, Pw, cbuf);
   return hipGetLastError() == hipSuccess ? MHE_OK : MHE_ERR_HIP;
+  }
 }
 
 // model dispatch: calls F.template operator()<DYN, MEAS>()
@@ -1339,8 +1367,17 @@ int dispatch(const mhe_dims* dm, F&& f) {
   switch (dm->dyn_model) {
     case MHE_DYN_VAN_DER_POL:
       if (dm->meas_model == MHE_MEAS_FULL_STATE) return f.template run<DynVanDerPol, MeasFullState<2>>();
+#ifndef MHE_FAST_BUILD
+      if (dm->meas_model == MHE_MEAS_MIXED) return f.template run<DynVanDerPol, MeasMixed<2>>();
+#endif
       break;
 #ifndef MHE_FAST_BUILD  // -DMHE_FAST_BUILD: van der Pol only (kernel development)
+    case MHE_DYN_MULTI_RECEIVER:
+      if (dm->meas_model == MHE_MEAS_MIXED) return f.template run<DynMultiReceiver, MeasMixed<8>>();
+      break;
+    case MHE_DYN_GNSS_TWO_RECEIVER:
+      if (dm->meas_model == MHE_MEAS_MIXED) return f.template run<DynGnssTwoReceiver, MeasMixed<10>>();
+      break;
     case MHE_DYN_SINGLE_INTEGRATOR:
       if (dm->meas_model == MHE_MEAS_FULL_STATE) return f.template run<DynSingleIntegrator, MeasFullState<1>>();
       break;
@@ -1350,9 +1387,11 @@ int dispatch(const mhe_dims* dm, F&& f) {
     case MHE_DYN_GNSS_POS_AND_BIAS:
       if (dm->meas_model == MHE_MEAS_PSEUDORANGE) return f.template run<DynGnssPosAndBias, MeasPseudorange<5>>();
       if (dm->meas_model == MHE_MEAS_FULL_STATE) return f.template run<DynGnssPosAndBias, MeasFullState<5>>();
+      if (dm->meas_model == MHE_MEAS_MIXED) return f.template run<DynGnssPosAndBias, MeasMixed<5>>();
       break;
     case MHE_DYN_KINEMATIC_BICYCLE:
       if (dm->meas_model == MHE_MEAS_PSEUDORANGE) return f.template run<DynKinematicBicycle, MeasPseudorange<6>>();
+      if (dm->meas_model == MHE_MEAS_MIXED) return f.template run<DynKinematicBicycle, MeasMixed<6>>();
       break;
     case MHE_DYN_DOUBLE_INTEGRATOR:
       if (dm->meas_model == MHE_MEAS_FULL_STATE) return f.template run<DynDoubleIntegrator, MeasFullState<4>>();
@@ -1414,6 +1453,7 @@ struct LaunchBig {
   BigArgs* a;
   int batch, max_iter;
   const double* X0;
+  const double* Z0;
   hipStream_t st;
   template <class DYN, class MEAS>
   int run() {
@@ -1430,11 +1470,20 @@ struct LaunchBig {
       return MHE_ERR_HIP;
     if (hipMemcpyAsync(A.X, X0, sizeof(double) * batch * A.P * A.n, hipMemcpyDeviceToDevice, st) != hipSuccess)
       return MHE_ERR_HIP;
+    if (A.nz > 0 && Z0 != A.Z &&
+        hipMemcpyAsync(A.Z, Z0, sizeof(double) * batch * A.nz, hipMemcpyDeviceToDevice, st) != hipSuccess)
+      return MHE_ERR_HIP;
+    const int K = A.nz + A.nc;
+    const int smem_b = (K * K + 2 * K) * (int)sizeof(double);
+    if (K > 0 && hipFuncSetAttribute((const void*)k_big_border<DYN::n>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     smem_b) != hipSuccess)
+      return MHE_ERR_HIP;
     hipLaunchKernelGGL(k_big_init, dim3((batch + 255) / 256), dim3(256), 0, st, batch, A.state, A.iters);
     for (int it = 0; it < max_iter; ++it) {
       hipLaunchKernelGGL((k_big_resid<DYN, MEAS>), dim3(batch), dim3(BIG_NTHREADS), 0, st, A, 0);
       hipLaunchKernelGGL((k_big_assemble<DYN, MEAS>), dim3((ntiles + 3) / 4, batch), dim3(256), 0, st, A);
       hipLaunchKernelGGL(k_big_chol, dim3(batch), dim3(BIG_NTHREADS), smem, st, A);
+      if (K > 0) hipLaunchKernelGGL(k_big_border<DYN::n>, dim3(batch), dim3(BIG_NTHREADS), smem_b, st, A);
       hipLaunchKernelGGL((k_big_update<DYN::n>), dim3(batch), dim3(256), 0, st, A);
     }
     hipLaunchKernelGGL((k_big_resid<DYN, MEAS>), dim3(batch), dim3(BIG_NTHREADS), 0, st, A, 1);
@@ -1444,7 +1493,7 @@ struct LaunchBig {
 };
 
 size_t big_ws_doubles(const mhe_dims* dm, int NT) {
-  return big_ws_layout(dm->N + 1, dm->M, dm->n, NT).total;
+  return big_ws_layout(dm->N + 1, dm->M, dm->n, NT, dm->n_extra, dm->n_eq).total;
 }
 
 }  // namespace
@@ -1473,7 +1522,7 @@ size_t mhe_workspace_bytes(const mhe_dims* dims, int32_t batch) {
 size_t mhe_const_bytes(const mhe_dims* dims) {
   int NT = 0;
   if (check_dims(dims, &NT) != MHE_OK) return 0;
-  if (is_big(dims)) return big_const_layout(dims->N + 1, dims->M, dims->n, dims->p).total;
+  if (is_big(dims)) return big_const_layout(dims->N + 1, dims->M, dims->n, dims->p, dims->n_eq).total;
   return const_layout(dims->N + 1, dims->M, dims->n, dims->p, NT).total;
 }
 
@@ -1501,13 +1550,23 @@ int mhe_gn_solve_ws(const mhe_dims* dims, const void* const_buf, int32_t batch, 
                     const double* U, int64_t u_bstride, const double* Y, const double* PAR, int64_t par_bstride,
                     const double* x0, double* cost_out, int32_t* iters_out, int32_t* status_out, int32_t max_iter,
                     double tol, void* workspace, size_t workspace_bytes, void* stream) {
+  return mhe_gn_solve_ext(dims, const_buf, batch, X0, X_out, nullptr, nullptr, U, u_bstride, Y, PAR, par_bstride, x0,
+                          cost_out, iters_out, status_out, max_iter, tol, workspace, workspace_bytes, stream);
+}
+
+int mhe_gn_solve_ext(const mhe_dims* dims, const void* const_buf, int32_t batch, const double* X0, double* X_out,
+                     const double* Z0, double* Z_out, const double* U, int64_t u_bstride, const double* Y,
+                     const double* PAR, int64_t par_bstride, const double* x0, double* cost_out, int32_t* iters_out,
+                     int32_t* status_out, int32_t max_iter, double tol, void* workspace, size_t workspace_bytes,
+                     void* stream) {
   int NT = 0;
   int rc = check_dims(dims, &NT);
   if (rc != MHE_OK) return rc;
   if (batch < 0 || max_iter < 0) return MHE_ERR_DIMS;
   if (batch == 0) return MHE_OK;
   if (!const_buf || !X0 || !X_out || !cost_out || !iters_out || !status_out || (dims->M > 0 && !Y) ||
-      (dims->m > 0 && !U) || (dims->q > 0 && !PAR) || (dims->has_prior && !x0))
+      (dims->m > 0 && !U) || (dims->q > 0 && !PAR) || (dims->has_prior && !x0) ||
+      (dims->n_extra > 0 && (!Z0 || !Z_out)))
     return MHE_ERR_NULL;
   if (is_big(dims)) {
     if (dims->dyn_cost != MHE_COST_L2) return MHE_ERR_UNSUPPORTED;  // Huber: fused path only (this build)
@@ -1527,7 +1586,10 @@ int mhe_gn_solve_ws(const mhe_dims* dims, const void* const_buf, int32_t batch, 
       A.blb[i] = dims->bound_lb[i];
       A.bub[i] = dims->bound_ub[i];
     }
-    LaunchBig f{dims, &A, batch, max_iter, X0, (hipStream_t)stream};
+    A.nz = dims->n_extra;
+    A.nc = dims->n_eq;
+    A.Z = Z_out;
+    LaunchBig f{dims, &A, batch, max_iter, X0, Z0, (hipStream_t)stream};
     return dispatch(dims, f);
   }
   GnArgs a = make_args(dims, const_buf, NT);

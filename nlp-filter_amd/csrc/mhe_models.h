@@ -8,6 +8,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "mhe.h"
+
 namespace mhe {
 
 // nlp/dynamics.py:4-8  xdot = u[0]
@@ -125,7 +127,7 @@ struct DynKinematicBicycle {
 template <int N_>
 struct MeasFullState {
   static constexpr int p = N_, q = 0;
-  static constexpr bool LINEAR = true;
+  static constexpr bool LINEAR = true, MIXED = false;
   __device__ static void eval(const double* x, const double*, const int*, double* h, double* H) {
 #pragma unroll
     for (int a = 0; a < p; ++a) {
@@ -140,7 +142,7 @@ struct MeasFullState {
 template <int N_>
 struct MeasPseudorange {
   static constexpr int p = 1, q = 3;
-  static constexpr bool LINEAR = false;
+  static constexpr bool LINEAR = false, MIXED = false;
   __device__ static void eval(const double* x, const double* par, const int* idx, double* h, double* H) {
     const double d0 = x[idx[0]] - par[0], d1 = x[idx[1]] - par[1], d2 = x[idx[2]] - par[2];
     const double rho = sqrt(d0 * d0 + d1 * d1 + d2 * d2);
@@ -159,7 +161,7 @@ struct MeasPseudorange {
 template <int N_>
 struct MeasRange3D {
   static constexpr int p = 1, q = 3;
-  static constexpr bool LINEAR = false;
+  static constexpr bool LINEAR = false, MIXED = false;
   __device__ static void eval(const double* x, const double* par, const int* idx, double* h, double* H) {
     const double d0 = x[idx[0]] - par[0], d1 = x[idx[1]] - par[1], d2 = x[idx[2]] - par[2];
     const double r = sqrt(d0 * d0 + d1 * d1 + d2 * d2 + 0.000001);
@@ -170,6 +172,82 @@ struct MeasRange3D {
     H[idx[0]] += d0 * ir;
     H[idx[1]] += d1 * ir;
     H[idx[2]] += d2 * ir;
+  }
+};
+
+// MHE_MEAS_MIXED: one scalar row of any of the reference plug-ins (include/mhe.h
+// documents the PAR row [code, i0..i6, v0..v5]).  x has N_ + MHE_MAX_EXTRA entries
+// ([x(t_i) ; z]), G (same length) receives dh/d[x ; z].  An index outside
+// [0, N_ + nz) contributes nothing (rows are device data: never read out of range).
+template <int N_>
+struct MeasMixed {
+  static constexpr int p = 1, q = MHE_MIXED_Q, NA = N_ + MHE_MAX_EXTRA;
+  static constexpr bool LINEAR = false, MIXED = true;
+  __device__ static void eval(const double* x, const double* par, int nz, double& h, double* G) {
+#pragma unroll
+    for (int c = 0; c < NA; ++c) G[c] = 0.0;
+    int id[7];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      const int v = (int)par[1 + k];
+      id[k] = (v >= 0 && v < N_ + nz) ? v : -1;
+    }
+    auto X = [&](int k) { return id[k] >= 0 ? x[id[k]] : 0.0; };
+    auto add = [&](int k, double g) {
+      if (id[k] >= 0) G[id[k]] += g;
+    };
+    const double* v = par + 8;
+    switch ((int)par[0]) {
+      case MHE_ROW_PSEUDORANGE: {  // nlp/measurements.py:56-70
+        const double d0 = X(0) - v[0], d1 = X(1) - v[1], d2 = X(2) - v[2];
+        const double rho = sqrt(d0 * d0 + d1 * d1 + d2 * d2);
+        h = rho + X(3);
+        add(0, d0 / rho); add(1, d1 / rho); add(2, d2 / rho); add(3, 1.0);
+        break;
+      }
+      case MHE_ROW_PSEUDORANGE_RATE: {  // nlp/measurements.py:72-79
+        const double r0 = v[0] - X(0), r1 = v[1] - X(1), r2 = v[2] - X(2);
+        const double nr = sqrt(r0 * r0 + r1 * r1 + r2 * r2);
+        const double l0 = r0 / nr, l1 = r1 / nr, l2 = r2 / nr;
+        const double w0 = v[3] - X(3), w1 = v[4] - X(4), w2 = v[5] - X(5);
+        const double wl = w0 * l0 + w1 * l1 + w2 * l2;
+        h = wl + X(6);
+        // d/dx_pos = -(w - (w.l) l) / |r|,  d/dx_vel = -l
+        add(0, -(w0 - wl * l0) / nr); add(1, -(w1 - wl * l1) / nr); add(2, -(w2 - wl * l2) / nr);
+        add(3, -l0); add(4, -l1); add(5, -l2); add(6, 1.0);
+        break;
+      }
+      case MHE_ROW_RANGE_2D:
+      case MHE_ROW_RANGE_3D: {  // nlp/measurements.py:7-20, 39-54
+        const int K = (int)par[0] == MHE_ROW_RANGE_2D ? 2 : 3;
+        double d[3] = {0.0, 0.0, 0.0}, s = 0.000001;
+        for (int k = 0; k < K; ++k) {
+          d[k] = X(k) - X(k + K) - v[k];
+          s += d[k] * d[k];
+        }
+        const double r = sqrt(s);
+        h = r;
+        for (int k = 0; k < K; ++k) {
+          add(k, d[k] / r);
+          add(k + K, -d[k] / r);
+        }
+        break;
+      }
+      case MHE_ROW_HEADING_2D: {  // nlp/measurements.py:22-37: atan2(r_x, r_y)
+        const double rx = X(0) - X(1) + v[0], ry = X(2) - X(3) + v[1];
+        const double q2 = rx * rx + ry * ry;
+        h = atan2(rx, ry);
+        add(0, ry / q2); add(1, -ry / q2); add(2, -rx / q2); add(3, rx / q2);
+        break;
+      }
+      case MHE_ROW_COMPONENT:  // nlp/measurements.py:4-5, one component
+        h = X(0);
+        add(0, 1.0);
+        break;
+      default:
+        h = 0.0;
+        break;
+    }
   }
 };
 

@@ -26,6 +26,7 @@ class MheDims(ctypes.Structure):
         ("meas_idx", c_i32 * 8), ("T", c_dbl),
         ("dyn_cost", c_i32), ("n_bounds", c_i32), ("huber_delta", c_dbl),
         ("bound_idx", c_i32 * 8), ("bound_lb", c_dbl * 8), ("bound_ub", c_dbl * 8),
+        ("n_extra", c_i32), ("n_eq", c_i32), ("eq_idx", ctypes.POINTER(c_i32)),
     ]
 
 
@@ -51,6 +52,8 @@ SIGNATURES = {
     "mhe_workspace_bytes": (c_sz, [_P, c_i32]),
     "mhe_gn_solve_ws": (ctypes.c_int, [_P, c_vp, c_i32, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp,
                                        c_vp, c_vp, c_vp, c_i32, c_dbl, c_vp, c_sz, c_vp]),
+    "mhe_gn_solve_ext": (ctypes.c_int, [_P, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64,
+                                        c_vp, c_vp, c_vp, c_vp, c_i32, c_dbl, c_vp, c_sz, c_vp]),
     "mhe_assemble": (ctypes.c_int, [_P, c_vp, c_i32, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp,
                                     c_vp, c_vp, c_vp, c_vp]),
     "mhe_chol_solve": (ctypes.c_int, [_P, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),

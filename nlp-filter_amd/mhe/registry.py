@@ -28,7 +28,19 @@ MEAS = {
     "pseudorange": (2, 1, 3, False),        # :56-70 (q: sat_pos)
     "vehicle_pseudorange": (3, 1, 3, False),  # :81-88
     "multi_receiver_range_3d": (4, 1, 3, False),  # :39-54 ("y" form)
+    # several scalar plug-ins in one problem; rows encoded per include/mhe.h
+    # (MHE_MEAS_MIXED, built by nlp.NLP from its addResidualCost calls)
+    "mixed": (5, 1, 14, False),
 }
+
+# MHE_ROW_* codes of the mixed-row encoding (include/mhe.h), by reference plug-in name
+ROW_CODES = {
+    "pseudorange": 1, "vehicle_pseudorange": 1, "pseudorange_rate": 2,
+    "multi_receiver_range_2d": 3, "multi_receiver_range_3d": 4, "multi_receiver_heading_2d": 5,
+    "full_state": 6,
+}
+MIXED_Q = 14
+MAX_EXTRA, MAX_EQ = 4, 48
 
 # (dynamics, measurement) pairs compiled into libmhe.so (dispatch() in mhe_gn.hip)
 COMPILED_PAIRS = {
@@ -39,6 +51,12 @@ COMPILED_PAIRS = {
     ("gnss_pos_and_bias", "full_state"),
     ("kinematic_bycicle_and_bias", "pseudorange"),
     ("double_integrator", "full_state"),
+    # mixed rows / extra variables / equality constraints (large-system path)
+    ("van_der_pol", "mixed"),
+    ("multi_receiver", "mixed"),
+    ("gnss_two_receiver", "mixed"),
+    ("gnss_pos_and_bias", "mixed"),
+    ("kinematic_bycicle_and_bias", "mixed"),
 }
 
 

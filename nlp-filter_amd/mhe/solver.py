@@ -56,10 +56,14 @@ class BatchSolver:
       meas_idx        static index parameters of the measurement model
       dyn_cost        "l2" (weighted_l2_norm) or "huber" (pseudo_huber_loss, IRLS; huber_delta)
       bounds          [(state component, lb, ub), ...] enforced by projected GN (addVarBounds)
+      n_extra         extra decision variables z (meas="mixed" rows may reference them)
+      eq              (K, 2) equality constraints v[a] - v[b] = 0 on the node-major state
+                      vector (b = -1: v[a] = 0), met by every GN step (bordered KKT solve)
+    With meas="mixed", PAR rows follow include/mhe.h (q = 14) and Rw is (M,) weights.
     """
 
     def __init__(self, N, T, dyn, meas, D, cw, Phi, Qw, Rw, Pw=None, meas_idx=None, device="cuda",
-                 dyn_cost="l2", huber_delta=None, bounds=None):
+                 dyn_cost="l2", huber_delta=None, bounds=None, n_extra=0, eq=None):
         self.lib = _lib.load()
         if not torch.cuda.is_available():
             raise _lib.MheLibraryError("no HIP device visible: the estimator has no CPU path")
@@ -94,6 +98,17 @@ class BatchSolver:
             dims.bound_lb[i] = -np.inf if lo is None else float(lo)
             dims.bound_ub[i] = np.inf if hi is None else float(hi)
         self.dyn_cost, self.huber_delta, self.bounds = dyn_cost, huber_delta, bounds
+        self.n_extra = int(n_extra)
+        if self.n_extra and mname != "mixed":
+            raise ValueError("extra variables enter mixed measurement rows only (meas='mixed')")
+        dims.n_extra = self.n_extra
+        self._eq = np.zeros(0, dtype=np.int32) if eq is None else np.ascontiguousarray(
+            np.asarray(eq, dtype=np.int32).reshape(-1, 2).ravel())
+        dims.n_eq = self._eq.size // 2
+        if dims.n_eq:
+            import ctypes
+            dims.eq_idx = self._eq.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))  # self._eq keeps it alive
+        self.n_eq = dims.n_eq
         self.dims = dims
         self.dp = self.lib.mhe_padded_dim(dims)
         if self.dp < 0:
@@ -159,16 +174,19 @@ class BatchSolver:
             self._ws = torch.empty(nb, dtype=torch.uint8, device=self.device)
         return self._ws, nb
 
-    def _gn(self, B, X, Xo, U_t, ustr, Y_t, PAR_t, pstr, x0_t, cost, iters, status, max_iter, tol, stream):
+    def _gn(self, B, X, Xo, U_t, ustr, Y_t, PAR_t, pstr, x0_t, cost, iters, status, max_iter, tol, stream,
+            Z=None, Zo=None):
         ws, nb = self._workspace(B)
-        rc = self.lib.mhe_gn_solve_ws(self.dims, _ptr(self.cbuf), B, _ptr(X), _ptr(Xo), _ptr(U_t), ustr, _ptr(Y_t),
-                                      _ptr(PAR_t), pstr, _ptr(x0_t), _ptr(cost), _ptr(iters), _ptr(status),
-                                      int(max_iter), float(tol), _ptr(ws), nb, _stream(stream))
-        _lib.check(rc, "mhe_gn_solve_ws")
+        rc = self.lib.mhe_gn_solve_ext(self.dims, _ptr(self.cbuf), B, _ptr(X), _ptr(Xo), _ptr(Z), _ptr(Zo),
+                                       _ptr(U_t), ustr, _ptr(Y_t), _ptr(PAR_t), pstr, _ptr(x0_t), _ptr(cost),
+                                       _ptr(iters), _ptr(status), int(max_iter), float(tol), _ptr(ws), nb,
+                                       _stream(stream))
+        _lib.check(rc, "mhe_gn_solve_ext")
 
     # ------------------------------------------------------------------ calls
-    def solve(self, X0, U, Y, PAR=None, x0=None, max_iter=20, tol=1e-10, stream=None, out=None):
-        """Gauss-Newton to convergence. Returns (X, cost, iters, status) device tensors."""
+    def solve(self, X0, U, Y, PAR=None, x0=None, max_iter=20, tol=1e-10, stream=None, out=None, Z0=None):
+        """Gauss-Newton to convergence. Returns (X, cost, iters, status) device tensors,
+        and the extra variables Z (B, n_extra) as a fifth element when n_extra > 0."""
         X, B, U_t, ustr, Y_t, PAR_t, pstr, x0_t = self._inputs(X0, U, Y, PAR, x0)
         if out is None:
             Xo = torch.empty_like(X)
@@ -177,7 +195,13 @@ class BatchSolver:
             status = torch.empty(B, dtype=torch.int32, device=self.device)
         else:
             Xo, cost, iters, status = out
-        self._gn(B, X, Xo, U_t, ustr, Y_t, PAR_t, pstr, x0_t, cost, iters, status, max_iter, tol, stream)
+        Z = Zo = None
+        if self.n_extra:
+            Z = _dev(np.zeros((B, self.n_extra)) if Z0 is None else Z0, self.device, (B, self.n_extra))
+            Zo = torch.empty_like(Z)
+        self._gn(B, X, Xo, U_t, ustr, Y_t, PAR_t, pstr, x0_t, cost, iters, status, max_iter, tol, stream, Z, Zo)
+        if self.n_extra:
+            return Xo, cost, iters, status, Zo
         return Xo, cost, iters, status
 
     def prepare(self, X0, U, Y, PAR=None, x0=None):

@@ -229,6 +229,17 @@ def gen_plugins(ref):
     out["cost_weighted_l2"] = np.array([float(np.squeeze(ref.cost_functions.weighted_l2_norm(v, {"Q": Q}))) for v in vs])
     out["cost_l2"] = np.array([float(np.squeeze(ref.cost_functions.l2_norm(v))) for v in vs])
     out["cost_huber"] = np.array([float(np.squeeze(ref.cost_functions.pseudo_huber_loss(v, {"Q": Q, "delta": 0.7}))) for v in vs])
+    # idxA/idxB forms of the 2-D receiver-pair models (gnss-multi-receiver.py:92-107)
+    for key, fn, jac in (("heading2d_AB", ref.measurements.multi_receiver_heading_2d, cdiff_jac),
+                         ("range2d_AB", ref.measurements.multi_receiver_range_2d, cstep_jac)):
+        xs = rng.normal(size=(64, 10)) * 10.0
+        ys, Hs = [], []
+        for x in xs:
+            y0, J = jac(lambda xx: fn(xx, {"idxA": [0, 1], "idxB": [5, 6]}), x)
+            ys.append(y0); Hs.append(J)
+        out[f"meas_{key}_x"] = xs
+        out[f"meas_{key}_y"] = np.stack(ys)
+        out[f"meas_{key}_H"] = np.stack(Hs)
     np.savez_compressed(os.path.join(OUT, "plugins.npz"), **out)
 
 

@@ -39,3 +39,32 @@ def test_host_side_entry_points_without_gpu():
     d.dyn_model, d.N = 5, 500  # beyond the register-resident limit: large-system path
     assert lib.mhe_padded_dim(d) == 2 * 512  # component-major, P padded to 16 per component
     assert lib.mhe_workspace_bytes(d, 2) > 2 * 8 * (64 * 65 // 2) * 256
+
+
+def test_general_problem_dims_validation():
+    """Extra variables / equality constraints / mixed rows: host-side checks."""
+    lib = _lib.load()
+    d = _lib.MheDims()
+    d.N, d.n, d.m, d.p, d.M, d.q, d.dyn_model, d.meas_model, d.T = 10, 10, 6, 1, 30, 14, 8, 5, 5.0  # mixed
+    assert lib.mhe_padded_dim(d) == 10 * 16           # always the large-system path
+    assert lib.mhe_workspace_bytes(d, 4) > 0
+    pairs = (ctypes.c_int32 * 22)(*[v for j in range(11) for v in (j * 10 + 2, j * 10 + 7)])
+    d.n_eq, d.eq_idx = 11, ctypes.cast(pairs, ctypes.POINTER(ctypes.c_int32))
+    assert lib.mhe_const_bytes(d) > 0
+    d.n_extra = 3
+    assert lib.mhe_padded_dim(d) == 160
+    d.n_extra = 5                                      # > MHE_MAX_EXTRA
+    assert lib.mhe_padded_dim(d) == -1
+    d.n_extra = 0
+    pairs[1] = 110                                     # index past P*n
+    assert lib.mhe_padded_dim(d) == -1
+    pairs[1] = 7
+    d.eq_idx = ctypes.POINTER(ctypes.c_int32)()        # NULL table
+    assert lib.mhe_padded_dim(d) == -1
+    d.eq_idx = ctypes.cast(pairs, ctypes.POINTER(ctypes.c_int32))
+    d.n_bounds, d.bound_idx[0], d.bound_lb[0], d.bound_ub[0] = 1, 0, -1.0, 1.0
+    assert lib.mhe_padded_dim(d) == -1                 # bounds + constraints: unsupported
+    d.n_bounds, d.n_eq = 0, 0
+    d.meas_model, d.q, d.n_extra = 2, 3, 2             # extra variables need mixed rows
+    d.dyn_model, d.n, d.m = 6, 5, 3
+    assert lib.mhe_padded_dim(d) == -1
