@@ -522,12 +522,12 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_chol(BigArgs a) {
 // definite), so LDL^T without pivoting is stable; a z component no row depends on
 // (zero pivot with a zero row) is held fixed (dz = 0), the minimum-norm choice.
 // Dynamic LDS: K*K (Schur) + 2K (rhs / w, pivot column) doubles.
-template <int n>
+template <int n, int p>
 __global__ __launch_bounds__(BIG_NTHREADS) void k_big_border(BigArgs a) {
   constexpr int NZX = MHE_MAX_EXTRA;
   const int b = blockIdx.x;
   if (a.state[b] != BIG_RUNNING) return;
-  const BigConst CL = big_const_layout(a.P, a.M, n, 1, a.nc);
+  const BigConst CL = big_const_layout(a.P, a.M, n, p, a.nc);  // p: the Rw section size
   const BigWs WL = big_ws_layout(a.P, a.M, n, a.NT, a.nz, a.nc);
   double* ws = a.ws + (size_t)b * a.ws_stride;
   const double* H = ws + WL.H;

@@ -1475,7 +1475,7 @@ struct LaunchBig {
       return MHE_ERR_HIP;
     const int K = A.nz + A.nc;
     const int smem_b = (K * K + 2 * K) * (int)sizeof(double);
-    if (K > 0 && hipFuncSetAttribute((const void*)k_big_border<DYN::n>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    if (K > 0 && hipFuncSetAttribute((const void*)k_big_border<DYN::n, MEAS::p>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      smem_b) != hipSuccess)
       return MHE_ERR_HIP;
     hipLaunchKernelGGL(k_big_init, dim3((batch + 255) / 256), dim3(256), 0, st, batch, A.state, A.iters);
@@ -1483,7 +1483,7 @@ struct LaunchBig {
       hipLaunchKernelGGL((k_big_resid<DYN, MEAS>), dim3(batch), dim3(BIG_NTHREADS), 0, st, A, 0);
       hipLaunchKernelGGL((k_big_assemble<DYN, MEAS>), dim3((ntiles + 3) / 4, batch), dim3(256), 0, st, A);
       hipLaunchKernelGGL(k_big_chol, dim3(batch), dim3(BIG_NTHREADS), smem, st, A);
-      if (K > 0) hipLaunchKernelGGL(k_big_border<DYN::n>, dim3(batch), dim3(BIG_NTHREADS), smem_b, st, A);
+      if (K > 0) hipLaunchKernelGGL((k_big_border<DYN::n, MEAS::p>), dim3(batch), dim3(BIG_NTHREADS), smem_b, st, A);
       hipLaunchKernelGGL((k_big_update<DYN::n>), dim3(batch), dim3(256), 0, st, A);
     }
     hipLaunchKernelGGL((k_big_resid<DYN, MEAS>), dim3(batch), dim3(BIG_NTHREADS), 0, st, A, 1);

@@ -1,5 +1,5 @@
 """Constraint plug-ins -- kingdwd/nlp-filter nlp/constraints.py (signature kept;
-equality constraints are not on the Gauss-Newton hot path)."""
+on the GPU path as constraint index pairs of the bordered GN step)."""
 
 
 def equality_constaint(x, params=None):

@@ -24,10 +24,20 @@ Kept semantics
   * ``addVarBounds`` on the state trajectory -> projected Gauss-Newton (steps are
     clipped to the box); bounds on other variables are checked after the solve
     (``self.solver["bounds_violated"]``)
+  * several measurement plug-ins in one problem (one ``addResidualCost`` call
+    each, gnss-multi-receiver.py:70-140), extra decision variables used inside
+    measurement params (``{"y": XA}``, multi-receiver.py:73,99) and
+    ``addEqConstraint(constraints.equality_constaint, [X[i][a], X[j][b]])``
+    (gnss-multi-receiver.py:76-78): encoded as MHE_MEAS_MIXED rows, extra
+    variables and constraint pairs (include/mhe.h) and solved with a bordered
+    (KKT) Gauss-Newton step on the large-system path -- the constraints hold after
+    every step.  Mixed rows carry scalar weights, so a full_state term in a mixed
+    problem needs a diagonal R.
 
-Not on the Gauss-Newton path yet (raise ``UnsupportedFeature``): inequality /
-equality constraints, mixed measurement models in one problem,
-and ``fixedTimeOptimalControlNLP`` (out of scope: the north star is the estimator).
+Not on the Gauss-Newton path (raise ``UnsupportedFeature``): inequality
+constraints, equality-constraint plug-ins other than ``equality_constaint``,
+constraints on extra variables, and ``fixedTimeOptimalControlNLP`` (out of
+scope: the north star is the estimator).
 """
 import time
 import warnings
@@ -51,8 +61,29 @@ class Var:
         self.value = None
         self.init = None
 
+    def __getitem__(self, k):
+        """Scalar element ``x[k]`` (CasADi MX indexing), e.g. for addEqConstraint."""
+        k = int(k)
+        if not -self.size <= k < self.size:
+            raise IndexError(f"{self!r}[{k}]")
+        return Elem(self, k % self.size)
+
+    def __len__(self):
+        return self.size
+
     def __repr__(self):
         return f"Var({self.name}_{self.idx}, n={self.size})"
+
+
+class Elem:
+    """One scalar of a decision variable (``X[i][k]``)."""
+    __slots__ = ("var", "k")
+
+    def __init__(self, var, k):
+        self.var, self.k = var, k
+
+    def __repr__(self):
+        return f"{self.var!r}[{self.k}]"
 
 
 class Param:
@@ -88,6 +119,7 @@ class NLP(object):
         self.sol = None
         self.solver = None
         self._bounds = []
+        self._eq = []
 
     def addVariables(self, N_var, n_var, lb=None, ub=None, name='x'):
         X = []
@@ -109,7 +141,15 @@ class NLP(object):
         raise UnsupportedFeature("inequality constraints are not on the Gauss-Newton path (SURVEY.md §8 f4)")
 
     def addEqConstraint(self, h, arguments, params=None):
-        raise UnsupportedFeature("equality constraints are not on the Gauss-Newton path (SURVEY.md §8 f4)")
+        """nlp/nlp.py:52-53 with the reference's only equality plug-in,
+        constraints.equality_constaint (args[0] - args[1] == 0), on scalar
+        elements ``X[i][k]`` of the state trajectory."""
+        if _fname(h) != "equality_constaint":
+            raise UnsupportedFeature(f"equality constraint plug-in {_fname(h)!r}: supported is equality_constaint")
+        args = list(arguments)
+        if len(args) != 2 or not all(isinstance(a, Elem) for a in args):
+            raise UnsupportedFeature("equality_constaint needs two scalar variable elements, e.g. [X[i][2], X[i][7]]")
+        self._eq.append((args[0], args[1]))
 
     def setParameter(self, p, val):
         if not isinstance(p, Param):
@@ -251,7 +291,10 @@ class fixedTimeOptimalEstimationNLP(NLP):
             self.setParameter(U[k], u_t(self.CPM.tau2t(self.CPM.tau[k])))
 
     def setMeasurement(self, Y, t_array, y_array):
-        """nlp/nlp.py:310-312"""
+        """nlp/nlp.py:310-312 (Y may be one parameter handle, as CasADi's Y[i] indexing
+        of a single MX parameter allows, gnss-multi-receiver.py:197)"""
+        if isinstance(Y, Param):
+            Y = [Y]
         for (i, t) in enumerate(t_array):
             self.setParameter(Y[i], np.asarray(y_array)[:, i])
 
@@ -276,6 +319,109 @@ class fixedTimeOptimalEstimationNLP(NLP):
         return [(c, lo, hi) for c, (lo, hi) in sorted(box.items()) if np.isfinite(lo) or np.isfinite(hi)]
 
     # ------------------------------------------------------------ assembly
+    _SIMPLE = ("full_state", "pseudorange", "vehicle_pseudorange", "multi_receiver_range_3d")
+
+    def _extra_vars(self):
+        """Decision variables other than the state trajectory that measurement params
+        reference (``{"y": XA}``) -- the z of the bordered solve -- in declaration
+        order: ([(Var, z offset)], total size).  Variables no cost term references
+        keep their initial value, as they would under IPOPT (zero gradient)."""
+        used = {id(v) for g in self._meas for v in g["params"].values() if isinstance(v, Var)}
+        out, off = [], 0
+        for vn in self.var_names:
+            v = self.w[vn]
+            if id(v) in used and not any(v is x for x in self._X):
+                out.append((v, off))
+                off += v.size
+        return out, off
+
+    def _is_general(self):
+        names = {_fname(g["h"]) for g in self._meas}
+        if len(names) != 1 or names.pop() not in self._SIMPLE:
+            return True
+        for g in self._meas:
+            par = g["params"]
+            if "idxA" in par or any(isinstance(v, Var) for v in par.values()):
+                return True
+        return False
+
+    def _state_index(self, e):
+        for j, x in enumerate(self._X):
+            if e.var is x:
+                return j * self.n + e.k
+        raise UnsupportedFeature(f"constraint on {e!r}: only elements of the state trajectory are supported")
+
+    def _eq_pairs(self):
+        return np.array([(self._state_index(a), self._state_index(b)) for a, b in self._eq], dtype=np.int32)
+
+    def _mixed_rows(self, zoff):
+        """MHE_MEAS_MIXED encoding (include/mhe.h) of every addResidualCost term:
+        (t (M,), rows (M,14), Rw (M,), Y (M,)), sorted by time (stable) so that
+        rows at one time form one epoch on the device."""
+        n = self.n
+
+        def vec(v, k):
+            return np.asarray(_resolve(v), dtype=np.float64).reshape(k)
+
+        def var_or_const(par, key, k):
+            y = par[key]
+            if isinstance(y, Var):
+                return [n + zoff[id(y)] + c for c in range(k)], np.zeros(k)
+            return [-1] * k, vec(y, k)
+
+        t_all, rows, Rw, Yv = [], [], [], []
+        for g in self._meas:
+            name, par, p = _fname(g["h"]), g["params"], g["p"]
+            R = np.asarray(_resolve(g["R"]), dtype=np.float64).reshape(p, p)
+            if name == "full_state":
+                if np.any(R != np.diag(np.diag(R))):
+                    raise UnsupportedFeature("full_state term in a mixed problem needs a diagonal R")
+                proto = [([6, a] + [-1] * 6, np.zeros(6), R[a, a]) for a in range(p)]
+            else:
+                if p != 1:
+                    raise UnsupportedFeature(f"{name}: scalar measurement expected, got p={p}")
+                v = np.zeros(6)
+                if name in ("pseudorange", "vehicle_pseudorange"):
+                    idx = list(par.get("idx", [0, 1, 2, 3])) if name == "pseudorange" else [0, 1, 8, 6]
+                    ids = [1] + idx + [-1] * 3
+                    v[:3] = vec(par["sat_pos"], 3)
+                elif name == "pseudorange_rate":
+                    ids = [2, 0, 1, 2, 4, 5, 6, 7]
+                    v[:3], v[3:6] = vec(par["sat_pos"], 3), vec(par["sat_vel"], 3)
+                elif name in ("multi_receiver_range_2d", "multi_receiver_range_3d"):
+                    K = 2 if name.endswith("2d") else 3
+                    code = 3 if K == 2 else 4
+                    if "y" in par:
+                        ia = list(par.get("idx", list(range(K))))[:K]
+                        ib, yv = var_or_const(par, "y", K)
+                        v[:K] = yv
+                    else:
+                        ia, ib = list(par["idxA"])[:K], list(par["idxB"])[:K]
+                    ids = [code] + ia + ib + [-1] * (7 - 2 * K)
+                elif name == "multi_receiver_heading_2d":
+                    if "y" in par:   # r_x = y0 - x[idx0], r_y = y1 - x[idx1]
+                        idx = list(par.get("idx", [0, 1]))
+                        yi, yv = var_or_const(par, "y", 2)
+                        ids = [5, yi[0], idx[0], yi[1], idx[1], -1, -1, -1]
+                        v[:2] = yv
+                    else:            # r_x = x[b0] - x[a0] + 1e-5, r_y = x[b1] - x[a1]
+                        a_, b_ = list(par["idxA"]), list(par["idxB"])
+                        ids = [5, b_[0], a_[0], b_[1], a_[1], -1, -1, -1]
+                        v[0] = .00001
+                else:
+                    raise UnsupportedFeature(f"measurement plug-in {name!r} has no mixed-row encoding")
+                proto = [(ids, v, R[0, 0])]
+            for i, t in enumerate(g["t"]):
+                yi = g["Y"][i].get()
+                for r, (ids, v, w) in enumerate(proto):
+                    t_all.append(t)
+                    rows.append(np.concatenate([np.asarray(ids, dtype=np.float64), v]))
+                    Rw.append(w)
+                    Yv.append(yi[r] if len(proto) > 1 else yi[0])
+        t_all = np.asarray(t_all)
+        order = np.argsort(t_all, kind="stable")
+        return t_all[order], np.stack(rows)[order], np.asarray(Rw)[order], np.asarray(Yv)[order]
+
     def _spec(self):
         if self._dyn is None:
             raise ValueError("addDynamics() must be called before build()")
@@ -284,9 +430,7 @@ class fixedTimeOptimalEstimationNLP(NLP):
         if not self._meas:
             raise ValueError("at least one addResidualCost() term is required")
         names = {_fname(g["h"]) for g in self._meas}
-        if len(names) != 1:
-            raise UnsupportedFeature(f"one measurement model per problem on the GPU path, got {sorted(names)}")
-        mname = names.pop()
+        mname = next(iter(names))
         t_meas, Rw, PAR, idx = [], [], [], None
         for g in self._meas:
             R = np.asarray(_resolve(g["R"]), dtype=np.float64).reshape(g["p"], g["p"])
@@ -297,8 +441,6 @@ class fixedTimeOptimalEstimationNLP(NLP):
                 if "idx" in par:
                     idx = list(par["idx"])
             elif mname == "multi_receiver_range_3d":
-                if "y" not in par:
-                    raise UnsupportedFeature("multi_receiver_range_3d between two state blocks (idxA/idxB)")
                 row_par = np.asarray(_resolve(par["y"]), dtype=np.float64).reshape(3)
                 idx = list(par.get("idx", [0, 1, 2]))
             for t in g["t"]:
@@ -311,20 +453,36 @@ class fixedTimeOptimalEstimationNLP(NLP):
     def build(self, verbose=True):
         """Build the device constants (nlp/nlp.py:61-69)."""
         from mhe import solver as _solver
-        mname, t_meas, Rw, PAR, idx = self._spec()
+        if self._dyn is None or self._dyn_cost is None or not self._meas:
+            self._spec()  # raises the precise error
         func = self._dyn[0]
-        Phi = self.CPM.lagrange_matrix(t_meas)
         Pw = None if self._prior is None else np.asarray(_resolve(self._prior[0]), dtype=np.float64)
         bounds = self._enforced_bounds()
         huber = getattr(self, "_huber", None)
-        key = (Rw.tobytes(), None if Pw is None else Pw.tobytes(), self._dyn_cost.tobytes(), huber, tuple(bounds))
+        extra, nz = self._extra_vars()
+        eq = self._eq_pairs() if self._eq else None
+        general = self._is_general() or nz > 0
+        if general:
+            if nz > 4:
+                raise UnsupportedFeature(f"{nz} extra decision variables (at most 4 on the GPU path)")
+            zoff = {id(v): off for v, off in extra}
+            t_meas, rows, Rw, Yv = self._mixed_rows(zoff)
+            mname, idx, PAR = "mixed", None, rows
+            self._Ymixed = Yv
+        else:
+            mname, t_meas, Rw, PAR, idx = self._spec()
+            self._Ymixed = None
+        Phi = self.CPM.lagrange_matrix(t_meas)
+        key = (mname, t_meas.tobytes(), Rw.tobytes(), None if Pw is None else Pw.tobytes(), self._dyn_cost.tobytes(),
+               huber, tuple(bounds), nz, None if eq is None else eq.tobytes())
         if self._engine is None or self._engine_key != key:
             self._engine = _solver.BatchSolver(self.N, self.T, func, mname, self.CPM.D, (self.T / 2.0) * self.CPM.w,
                                                Phi, self._dyn_cost, Rw, Pw=Pw, meas_idx=idx, device=self.device,
                                                dyn_cost="huber" if huber is not None else "l2", huber_delta=huber,
-                                               bounds=bounds)
+                                               bounds=bounds, n_extra=nz, eq=eq)
             self._engine_key = key
         self._PAR = PAR
+        self._extra = extra
 
     def batch_solver(self):
         """The BatchSolver of this problem structure (many trajectories at once)."""
@@ -337,30 +495,45 @@ class fixedTimeOptimalEstimationNLP(NLP):
         """Gauss-Newton on the GPU (replaces opti.solve(), nlp/nlp.py:76-83)."""
         if warmstart and self.sol is not None:
             print('Warmstarting with previous solution')
-        self.build()  # cheap when nothing changed; picks up re-set R / prior weights
+        self.build()  # cheap when nothing changed; picks up re-set R / prior weights / params
         eng = self._engine
         P, n = self.N + 1, self.n
+
+        def start(x):
+            if warmstart and self.sol is not None and x.value is not None:
+                return x.value
+            return x.init if x.init is not None else 0.0  # CasADi's default initial value
+
         X0 = np.zeros((1, P, n))
         for k, x in enumerate(self._X):
-            if warmstart and self.sol is not None and x.value is not None:
-                X0[0, k] = x.value
-            elif x.init is not None:
-                X0[0, k] = x.init
+            X0[0, k] = start(x)
+        Z0 = None
+        if eng.n_extra:
+            Z0 = np.concatenate([np.broadcast_to(np.asarray(start(v), dtype=np.float64).reshape(-1), (v.size,))
+                                 for v, _ in self._extra])[None]
         U = None
         if self.m > 0:
             U = np.stack([u.get() for u in self._dyn[2]])[None]
-        Y = np.concatenate([np.stack([y.get() for y in g["Y"]]) for g in self._meas])[None]
+        if self._Ymixed is not None:
+            Y = self._Ymixed.reshape(1, -1, 1)
+        else:
+            Y = np.concatenate([np.stack([y.get() for y in g["Y"]]) for g in self._meas])[None]
         PAR = None if self._PAR is None else self._PAR[None]
         x0 = None if self._prior is None else self._prior[1].get()[None]
         import torch
         t0 = time.perf_counter()
-        X, cost, iters, status = eng.solve(X0, U, Y, PAR, x0, max_iter=self.max_iter, tol=self.tol)
+        out = eng.solve(X0, U, Y, PAR, x0, max_iter=self.max_iter, tol=self.tol, Z0=Z0)
+        X, cost, iters, status = out[:4]
         torch.cuda.synchronize()
         t_wall = time.perf_counter() - t0
         X = X.cpu().numpy()[0]
         st = int(status.cpu().numpy()[0])
         for k, x in enumerate(self._X):
             x.value = X[k].copy()
+        if eng.n_extra:
+            Z = out[4].cpu().numpy()[0]
+            for v, off in self._extra:
+                v.value = Z[off:off + v.size].copy()
         # W eliminated: W_k = (2/T) sum_j D_kj X_j - f(X_k, U_k)  (nlp/nlp.py:235)
         func, dparams, Uh, W = self._dyn
         for k, wv in enumerate(W):

@@ -117,3 +117,168 @@ def multi_receiver_problem(N=7, T=6.0, B=2, seed=1):
     Z0 = zt + rng.normal(size=zt.shape) * 0.5
     Z0[:, 2] = 7.0   # unobservable: must stay where it starts
     return pb, X0, Z0, None, Y, np.tile(rows[None], (B, 1, 1)), xt, zt
+
+
+# ---------------------------------------------------------------------------
+# gnss-multi-receiver.py (two receivers, 96 MHE windows) restated on the oracle
+TWO_RX = dict(T=5.0, N=10, n=10, m=6, r_pr_A=10.0, r_pr_B=1.0, r_range=0.01, r_heading=0.1,
+              distance=0.5 * 91.44, heading=-44.0, dt_range=0.1, dt_heading=0.1, dt_gnss=1.0, N_sat=10, DT=1.0)
+
+
+def two_rx_weights():
+    """gnss-multi-receiver.py:44-50"""
+    Q = np.diag([.01, .01, .01, 0.01, 0.01, .01, .01, .01, 0.01, 0.01])
+    P = 0.01 * np.diag([1, 1, 1, 0.1, 0.1, 1, 1, 1, 0.1, 0.1])
+    return np.linalg.inv(Q), np.linalg.inv(P)
+
+
+def two_rx_window_rows(c, satA, prA, satB, prB):
+    """Rows of one window in the script's addResidualCost order (:63-123): range_3d at
+    t_range, heading_2d at t_heading, then per GNSS epoch i and slot j < N_sat the
+    pseudoranges of A and B (R = 0 and zero inputs for empty slots, :186-204).
+    satX[i] (k_i, 3) ENU satellite positions and prX[i] (k_i,) of the window's epochs.
+    Returns (t, rows (M,14), Rw (M,), Y (M,))."""
+    T = c["T"]
+    t_range = np.linspace(0, T, int(np.floor(T / c["dt_range"])) + 1)
+    t_head = np.linspace(0, T, int(np.floor(T / c["dt_heading"])) + 1)
+    t_gnss = np.linspace(0, T, int(np.floor(T / c["dt_gnss"])) + 1)
+    t, rows, Rw, Y = [], [], [], []
+    for tt in t_range:
+        t.append(tt); rows.append(row(gg.ROW_R3, [0, 1, 2, 5, 6, 7]))
+        Rw.append(c["dt_range"] * (1.0 / c["r_range"])); Y.append(c["distance"])
+    for tt in t_head:
+        t.append(tt); rows.append(row(gg.ROW_HEAD, [5, 0, 6, 1], [1e-5, 0.0]))
+        Rw.append(c["dt_heading"] * (1.0 / c["r_heading"])); Y.append(np.deg2rad(c["heading"]))
+    for i, tt in enumerate(t_gnss):
+        for j in range(c["N_sat"]):
+            for sat, pr, base, r in ((satA, prA, 0, c["r_pr_A"]), (satB, prB, 5, c["r_pr_B"])):
+                if j < sat[i].shape[0]:
+                    t.append(tt); rows.append(row(gg.ROW_PR, [base, base + 1, base + 2, base + 3], sat[i][j]))
+                    Rw.append(c["dt_gnss"] * (1.0 / r)); Y.append(pr[i][j])
+                else:
+                    t.append(tt); rows.append(row(gg.ROW_PR, [base, base + 1, base + 2, base + 3], np.zeros(3)))
+                    Rw.append(0.0); Y.append(0.0)
+    return np.array(t), np.array(rows), np.array(Rw), np.array(Y)
+
+
+def two_rx_mhe_oracle(dA, dB, lsA, lsB, p_ref, n_windows, enu, max_iter=50, tol=1e-10, overrides=None, with_eq=True):
+    """gnss-multi-receiver.py:142-244 on the oracle.  dA/dB: load_gnss_logs dicts,
+    lsA/lsB: runLeastSquares-style dicts with x/y/z_ENU, xd/yd/zd_ENU, bias;
+    enu(p_ecef) -> ENU at p_ref.  Returns per window the state at t = T (x_opt[49])
+    and at t = DT, plus per-window GN status."""
+    from scipy.interpolate import interp1d
+    c = dict(TWO_RX, **(overrides or {}))
+    T, N, n, DT = c["T"], c["N"], c["n"], c["DT"]
+    P = N + 1
+    Qw, Pw = two_rx_weights()
+    D, cw = oc.diff_matrix(N), (T / 2.0) * oc.quad_weights(N)
+    t_nodes = oc.tau2t(oc.nodes(N), 0.0, T)
+    eq = np.array([[k * n + 2, k * n + 7] for k in range(P)])
+    xhat0 = np.array([lsA["x_ENU"][0], lsA["y_ENU"][0], lsA["z_ENU"][0], lsA["bias"][0], 0.0,
+                      lsB["x_ENU"][0], lsB["y_ENU"][0], lsB["z_ENU"][0], lsB["bias"][0], 0.0])
+    tA, tB = np.asarray(dA["t"], dtype=np.float64), np.asarray(dB["t"], dtype=np.float64)
+    t_off = tB[0] - tA[0]
+    X = np.zeros((1, P, n))
+    out_T, out_DT, status = [], [], []
+    for step, t0 in enumerate(np.linspace(0, n_windows - 1, n_windows) * DT):
+        iA = np.nonzero((tA >= t0) & (tA <= t0 + T))[0]
+        iB = np.nonzero((tB >= t0 + t_off) & (tB <= t0 + t_off + T))[0]
+        sA, sB = tA[iA] - t0, tB[iB] - t0 - t_off
+        uA = np.vstack([lsA[k][iA] for k in ("xd_ENU", "yd_ENU", "zd_ENU")])
+        uB = np.vstack([lsB[k][iB] for k in ("xd_ENU", "yd_ENU", "zd_ENU")])
+        uB = interp1d(sB, uB, fill_value="extrapolate")(sA)
+        U = interp1d(sA, np.vstack((uA, uB)), fill_value="extrapolate")(t_nodes).T[None]
+        satA = [np.array([enu(s) for s in dA["sat_pos"][k]]).reshape(-1, 3) for k in iA]
+        satB = [np.array([enu(s) for s in dB["sat_pos"][k]]).reshape(-1, 3) for k in iB]
+        t, rows, Rw, Y = two_rx_window_rows(c, satA, [dA["pr"][k] for k in iA], satB, [dB["pr"][k] for k in iB])
+        order = np.argsort(t, kind="stable")
+        t, rows, Rw, Y = t[order], rows[order], Rw[order], Y[order]
+        pb = gg.GeneralProblem(N, T, n, 6, "gnss_two_receiver", "mixed", D, cw, oc.interp_matrix(N, T, t), Qw, Rw,
+                               Pw=Pw, eq=eq if with_eq else None)
+        X, _, _, _, st = gg.gauss_newton_general(pb, X, None, U, Y.reshape(1, -1, 1), rows[None], xhat0[None],
+                                                 max_iter=max_iter, tol=tol)
+        status.append(int(st[0]))
+        out_T.append(oc.interp_matrix(N, T, [T])[0] @ X[0])
+        xhat0 = oc.interp_matrix(N, T, [DT])[0] @ X[0]
+        out_DT.append(xhat0)
+    return np.array(out_T), np.array(out_DT), np.array(status)
+
+
+def two_rx_mhe_facade(dA, dB, lsA, lsB, p_ref, n_windows, overrides=None):
+    """gnss-multi-receiver.py:38-244 written against THIS package's facade (nlp.nlp,
+    its plug-in modules, utils.utils) -- the same calls in the same order.  Returns
+    per window x_opt at t = T and xhat0 at t = DT, plus the GN status string."""
+    from nlp import constraints, cost_functions, dynamics, measurements
+    from nlp import nlp as nlpmod
+    from utils import utils as gu
+    c = dict(TWO_RX, **(overrides or {}))
+    Qi, Pi = two_rx_weights()
+    T, N, n, m = c["T"], c["N"], c["n"], c["m"]
+    problem = nlpmod.fixedTimeOptimalEstimationNLP(N, T, n, m)
+    X = problem.addVariables(N + 1, n, name='x')
+    U, W = problem.addDynamics(dynamics.gnss_two_receiver, X, None, None)
+    problem.addDynamicsCost(cost_functions.weighted_l2_norm, W, {"Q": Qi})
+    X0 = problem.addInitialCost(cost_functions.weighted_l2_norm, X[0], {"Q": Pi})
+    t_range = np.linspace(0, T, int(np.floor(T / c["dt_range"])) + 1)
+    problem.addResidualCost(measurements.multi_receiver_range_3d, X, t_range,
+                            c["distance"] * np.ones((1, t_range.shape[0])),
+                            c["dt_range"] * np.array([1. / c["r_range"]]), {"idxA": [0, 1, 2], "idxB": [5, 6, 7]})
+    for i in range(N + 1):
+        problem.addEqConstraint(constraints.equality_constaint, [X[i][2], X[i][7]])
+    t_heading = np.linspace(0, T, int(np.floor(T / c["dt_heading"])) + 1)
+    problem.addResidualCost(measurements.multi_receiver_heading_2d, X, t_heading,
+                            np.deg2rad(c["heading"]) * np.ones((1, t_heading.shape[0])),
+                            c["dt_heading"] * np.array([1. / c["r_heading"]]), {"idxA": [0, 1], "idxB": [5, 6]})
+    N_gnss = int(np.floor(T / c["dt_gnss"]))
+    t_gnss = np.linspace(0, T, N_gnss + 1)
+    R_A, Y_A, S_A, R_B, Y_B, S_B = [], [], [], [], [], []
+    for i in range(N_gnss + 1):
+        t_i = np.array([[t_gnss[i]]])
+        rows = ([], [], [], [], [], [])
+        for j in range(c["N_sat"]):
+            for base, (Ys, Rs, Ss) in ((0, rows[0:3]), (5, rows[3:6])):
+                sp = problem.addParameter(1, 3)[0]
+                Rp = problem.addParameter(1, 1)[0]
+                Yp = problem.addResidualCost(measurements.pseudorange, X, t_i, None, Rp,
+                                             {"p": 1, "sat_pos": sp, "idx": [base, base + 1, base + 2, base + 3]})[0]
+                Ys.append(Yp); Rs.append(Rp); Ss.append(sp)
+        Y_A.append(rows[0]); R_A.append(rows[1]); S_A.append(rows[2])
+        Y_B.append(rows[3]); R_B.append(rows[4]); S_B.append(rows[5])
+    problem.build()
+    xhat0 = np.array([lsA["x_ENU"][0], lsA["y_ENU"][0], lsA["z_ENU"][0], lsA["bias"][0], 0.0,
+                      lsB["x_ENU"][0], lsB["y_ENU"][0], lsB["z_ENU"][0], lsB["bias"][0], 0.0])
+    DT = c["DT"]
+    tA, tB = np.asarray(dA["t"], dtype=np.float64), np.asarray(dB["t"], dtype=np.float64)
+    t_offset = tB[0] - tA[0]
+    out_T, out_DT, status = [], [], []
+    from scipy.interpolate import interp1d
+    for step, t0 in enumerate(np.linspace(0, (n_windows - 1) * DT, n_windows)):
+        iA = gu.get_time_indices(tA, t0, t0 + T)
+        iB = gu.get_time_indices(tB, t0 + t_offset, t0 + t_offset + T)
+        sA, sB = tA[iA] - t0, tB[iB] - t0 - t_offset
+        uA = np.vstack([lsA[k][iA].reshape(1, -1) for k in ("xd_ENU", "yd_ENU", "zd_ENU")])
+        uB = np.vstack([lsB[k][iB].reshape(1, -1) for k in ("xd_ENU", "yd_ENU", "zd_ENU")])
+        uB = interp1d(sB, uB, fill_value="extrapolate")(sA)
+        problem.setControl(U, sA, np.vstack((uA, uB)))
+        problem.setParameter(X0, xhat0)
+        for d, idxs, Ys, Rs, Ss, r in ((dA, iA, Y_A, R_A, S_A, c["r_pr_A"]), (dB, iB, Y_B, R_B, S_B, c["r_pr_B"])):
+            for i in range(N_gnss + 1):
+                k = idxs[i]
+                t_i = np.array([[t_gnss[i]]])
+                ns = d["sat_pos"][k].shape[0]
+                for j in range(c["N_sat"]):
+                    if j < ns:
+                        problem.setParameter(Rs[i][j], c["dt_gnss"] * np.linalg.inv(np.diag([r])))
+                        problem.setParameter(Ss[i][j], gu.ecef2enu(d["sat_pos"][k][j, :], p_ref))
+                        problem.setMeasurement(Ys[i][j], t_i, np.array([[d["pr"][k][j]]]))
+                    else:
+                        problem.setParameter(Rs[i][j], 0.0)
+                        problem.setParameter(Ss[i][j], np.zeros(3))
+                        problem.setMeasurement(Ys[i][j], t_i, np.array([[0.0]]))
+        problem.solve(warmstart=True)
+        x_opt = problem.extractSolution('x', np.linspace(0, T, 50))
+        xhat0 = problem.extractSolution('x', [DT])[0]
+        out_T.append(x_opt[-1])
+        out_DT.append(xhat0)
+        status.append(problem.solver["return_status"])
+    return np.array(out_T), np.array(out_DT), status
