@@ -219,9 +219,10 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_resid(BigArgs a, int final
       for (int c = 0; c < NZX * NZX; ++c) Hzz[c] = 0.0;
       for (int i = erow[e]; i < erow[e + 1]; ++i) {
         const double* PR = a.PAR + (long long)b * a.pstride + (long long)i * q;
+        const double R = Rw[i];
+        if (R == 0.0) continue;  // R = 0 masks the row (empty satellite slot, autonomous-car.py:260-263)
         double h, Gr[NA];
         MEAS::eval(xt, PR, nz, h, Gr);
-        const double R = Rw[i];
         const double ev = a.Y[(long long)b * a.M + i] - h, Re = R * ev;
         cost += ev * Re;
         for (int c = 0; c < n; ++c) {
@@ -257,10 +258,11 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_resid(BigArgs a, int final
         const double* PR = a.PAR + (long long)b * a.pstride + (long long)i * q;
         for (int c = 0; c < q; ++c) par[c] = PR[c];
       }
+      const double* R = Rw + (size_t)i * p * p;
+      if (masked_row<p>(R)) continue;  // R = 0 masks the row (autonomous-car.py:260-263)
       double h[p], Hm[p * n];
       MEAS::eval(xe, par, a.idx, h, Hm);
       const double* yi = a.Y + ((long long)b * a.M + i) * p;
-      const double* R = Rw + (size_t)i * p * p;
       double ev[p], Re[p];
       for (int r = 0; r < p; ++r) ev[r] = yi[r] - h[r];
       for (int r = 0; r < p; ++r) {

@@ -415,13 +415,19 @@ __device__ __forceinline__ double meas_phase(const GnArgs& a, const ConstLayout&
 #pragma unroll
       for (int c = 0; c < q; ++c) par[c] = PR[c];
     }
+    const double* R = Rw + (long long)i * p * p;
     double h[p], H[p * n];
     MEAS::eval(xi, par, a.idx, h, H);
     const double* yi = a.Y + ((long long)b * a.M + i) * p;
-    const double* R = Rw + (long long)i * p * p;
     double e[p], Re[p];
 #pragma unroll
     for (int r = 0; r < p; ++r) e[r] = yi[r] - h[r];
+    if (masked_row<p>(R)) {  // R = 0 masks the row (autonomous-car.py:260-263): no NaN from h at a singular point
+#pragma unroll
+      for (int c = 0; c < p * n; ++c) H[c] = 0.0;
+#pragma unroll
+      for (int r = 0; r < p; ++r) e[r] = 0.0;
+    }
 #pragma unroll
     for (int r = 0; r < p; ++r) {
       double s = 0.0;

@@ -175,6 +175,16 @@ struct MeasRange3D {
   }
 };
 
+// A measurement row whose weight matrix is all zero contributes nothing (the reference
+// masks empty satellite slots with R = 0, autonomous-car.py:260-263, gnss-multi-receiver.py:196-204).
+template <int p>
+__device__ __forceinline__ bool masked_row(const double* R) {
+  bool z = true;
+#pragma unroll
+  for (int c = 0; c < p * p; ++c) z = z && R[c] == 0.0;
+  return z;
+}
+
 // MHE_MEAS_MIXED: one scalar row of any of the reference plug-ins (include/mhe.h
 // documents the PAR row [code, i0..i6, v0..v5]).  x has N_ + MHE_MAX_EXTRA entries
 // ([x(t_i) ; z]), G (same length) receives dh/d[x ; z].  An index outside

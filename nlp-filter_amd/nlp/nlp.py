@@ -86,6 +86,10 @@ class Elem:
         return f"{self.var!r}[{self.k}]"
 
 
+class ParameterNotSet(ValueError):
+    """A parameter (or measurement slot) was read before setParameter()/setMeasurement()."""
+
+
 class Param:
     """Parameter handle (stands in for ``opti.parameter(n)``)."""
     __slots__ = ("size", "value")
@@ -96,7 +100,7 @@ class Param:
 
     def get(self):
         if self.value is None:
-            raise ValueError("parameter used before setParameter()")
+            raise ParameterNotSet("parameter used before setParameter()")
         return self.value
 
 
@@ -451,7 +455,17 @@ class fixedTimeOptimalEstimationNLP(NLP):
         return mname, np.asarray(t_meas), np.stack(Rw), (np.stack(PAR) if PAR else None), idx
 
     def build(self, verbose=True):
-        """Build the device constants (nlp/nlp.py:61-69)."""
+        """Build the device constants (nlp/nlp.py:61-69).  As with the reference, build()
+        may come before setParameter()/setMeasurement() (gnss-multi-receiver.py:142 vs
+        :200-230): constants that depend on unset parameters are then built by solve()."""
+        if self._dyn is None or self._dyn_cost is None or not self._meas:
+            self._spec()  # raises the precise structural error
+        try:
+            self._build()
+        except ParameterNotSet:
+            self._engine_key = None
+
+    def _build(self):
         from mhe import solver as _solver
         if self._dyn is None or self._dyn_cost is None or not self._meas:
             self._spec()  # raises the precise error
@@ -487,7 +501,7 @@ class fixedTimeOptimalEstimationNLP(NLP):
     def batch_solver(self):
         """The BatchSolver of this problem structure (many trajectories at once)."""
         if self._engine is None:
-            self.build()
+            self._build()
         return self._engine
 
     # ------------------------------------------------------------ solve
@@ -495,7 +509,7 @@ class fixedTimeOptimalEstimationNLP(NLP):
         """Gauss-Newton on the GPU (replaces opti.solve(), nlp/nlp.py:76-83)."""
         if warmstart and self.sol is not None:
             print('Warmstarting with previous solution')
-        self.build()  # cheap when nothing changed; picks up re-set R / prior weights / params
+        self._build()  # cheap when nothing changed; picks up re-set R / prior weights / params
         eng = self._engine
         P, n = self.N + 1, self.n
 

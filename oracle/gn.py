@@ -69,13 +69,21 @@ def residuals(pb, X, U, Y, PAR=None, x0=None):
         cost = np.einsum("k,bka,ac,bkc->b", pb.c, W, pb.Qw, W)
     xi = np.einsum("ij,bja->bia", pb.Phi, X)
     h, _ = models.meas_eval(pb.meas, xi, PAR, pb.meas_static)
-    e = Y - h
     Rw = pb.Rw if pb.Rw.ndim == 4 else pb.Rw[None]
+    with np.errstate(invalid="ignore"):
+        e = np.where(masked_rows(Rw)[..., None], 0.0, Y - h)
     cost = cost + np.einsum("bip,bipq,biq->b", e, np.broadcast_to(Rw, e.shape + (e.shape[-1],)), e)
     if pb.Pw is not None:
         r0 = X[:, 0] - x0
         cost = cost + np.einsum("ba,ac,bc->b", r0, pb.Pw, r0)
     return W, xi, e, cost
+
+
+def masked_rows(Rw):
+    """(B|1, M) True where a row's weight matrix is all zero: the reference masks empty
+    satellite slots with R = 0 (autonomous-car.py:260-263, gnss-multi-receiver.py:196-204),
+    so such a row contributes nothing -- even where h or its Jacobian is singular there."""
+    return np.all(Rw.reshape(Rw.shape[:2] + (int(np.prod(Rw.shape[2:])),)) == 0.0, axis=-1)
 
 
 def normal_equations(pb, X, U, Y, PAR=None, x0=None):
@@ -108,6 +116,7 @@ def normal_equations(pb, X, U, Y, PAR=None, x0=None):
     # measurements
     _, Hm = models.meas_eval(pb.meas, xi, PAR, pb.meas_static)    # (B,M,p,n)
     Rw = pb.Rw if pb.Rw.ndim == 4 else np.broadcast_to(pb.Rw[None], (B,) + pb.Rw.shape)
+    Hm = np.where(masked_rows(Rw)[..., None, None], 0.0, Hm)
     G = np.einsum("zipa,zipq,ziqc->ziac", Hm, Rw, Hm)              # (B,M,n,n)
     H4 += np.einsum("ij,il,ziac->zjalc", pb.Phi, pb.Phi, G)
     ge = np.einsum("zipa,zipq,ziq->zia", Hm, Rw, e)
@@ -156,6 +165,8 @@ def normal_equations_explicit(pb, X, U, Y, PAR=None, x0=None):
         for i in range(pb.M):  # measurement rows, nlp/nlp.py:264-273
             xi = pb.Phi[i] @ X[b]
             par = None if PAR is None else PAR[min(b, PAR.shape[0] - 1), i]
+            if not np.any(Rw[i]):
+                continue  # R = 0 masks the row (autonomous-car.py:260-263)
             hi, Hi = models.meas_eval(pb.meas, xi, par, pb.meas_static)
             A = np.zeros((Hi.shape[0], d))
             for j in range(P):

@@ -127,6 +127,8 @@ def normal_equations_full(pb, X, Z, U, Y, PAR, x0=None):
     for b in range(B):
         Rw = pb.Rw[b] if pb.Rw.ndim == 2 else pb.Rw
         for i in range(pb.M):
+            if float(np.ravel(Rw[i])[0]) == 0.0:
+                continue  # R = 0 masks the row (gnss-multi-receiver.py:196-204)
             xi = pb.Phi[i] @ X[b]
             xt = np.concatenate([xi, Z[b]])
             par = PAR[min(b, PAR.shape[0] - 1), i]

@@ -103,3 +103,19 @@ def test_facade_gnss_per_row_residual_costs():
     Xs = np.stack([problem.extractVariableValue('x', k) for k in range(w.N + 1)])
     assert sr[0] == 0 and problem.solver["success"]
     assert np.abs(Xs - Xr[0]).max() <= 1e-6 * (1 + np.abs(Xr).max())
+
+
+def test_build_before_set_parameter_is_deferred():
+    """gnss-multi-receiver.py calls problem.build() before any setParameter()/
+    setMeasurement(); build() must defer the parameter-dependent constants to solve()."""
+    w = configs.make_c1()
+    problem = nlp.fixedTimeOptimalEstimationNLP(w.N, w.T, w.n, w.m)
+    X = problem.addVariables(w.N + 1, w.n, name='x')
+    _, W = problem.addDynamics(dynamics.single_integrator, X, w.t_meas, np.sin(w.t_meas)[None, :])
+    problem.addDynamicsCost(cost_functions.weighted_l2_norm, W, {"Q": w.Qw})
+    Rp = problem.addParameter(1, 1)[0]
+    problem.addResidualCost(measurements.full_state, X, w.t_meas[:3], None, Rp, {"p": 1})
+    problem.build()                       # no error, nothing built yet
+    assert problem._engine is None and problem._engine_key is None
+    with pytest.raises(nlp.ParameterNotSet):
+        problem._build()                  # what solve() would hit with the parameter still unset
