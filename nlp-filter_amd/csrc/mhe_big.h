@@ -109,7 +109,6 @@ struct BigArgs {
   double tol;
   double* ws;      // workspace base
   size_t ws_stride;  // doubles per trajectory
-  int cache_tiles;   // block-column tiles cached in LDS by k_big_chol
   int n_bounds;      // projected GN (addVarBounds)
   int bidx[8];
   double blb[8], bub[8];
@@ -390,6 +389,25 @@ __global__ __launch_bounds__(256) void k_big_assemble(BigArgs a) {
 }
 
 // ------------------------------------------------------------ factor + solve
+// Blocked right-looking Cholesky over super-blocks of BIG_KB tile columns
+// (nb = 16 BIG_KB).  Per super-block:
+//   panel phase   the block column, 16 columns at a time: single-wave diagonal
+//                 panel (L_kk^-T, y_k), MFMA TRSM of the tiles below, updates
+//                 restricted to the block column's own tiles;
+//   trailing      A_IJ -= sum_{k in block} L_Ik L_Jk^T for all J >= block end:
+//                 K = nb per tile visit, so every trailing tile is read and
+//                 written once per nb columns instead of once per 16 (the 16-wide
+//                 right-looking form moved ~4x the HBM bytes for the same flops).
+//                 L_J of four tile columns is staged in LDS (B operands, shared by
+//                 all waves); each wave walks tile rows I, holds L_I (A operands)
+//                 in registers and updates the row's (up to) four tiles.
+constexpr int BIG_KB = 8;      // tile columns per super-block
+constexpr int BIG_JB = 8;      // tile columns per LDS-staged trailing slab
+#ifndef MHE_BIG_KO
+#define MHE_BIG_KO 0  // knock-out mask for timing probes only (tools/ko_big.sh): 1 trailing, 2 in-block, 4 TRSM
+#endif
+constexpr int BIG_CHOL_LDS = DTS + BIG_NW * 16 + 16 + 2 + BIG_JB * BIG_KB * 256;  // doubles
+
 __global__ __launch_bounds__(BIG_NTHREADS) void k_big_chol(BigArgs a) {
   const int b = blockIdx.x;
   if (a.state[b] != BIG_RUNNING) return;
@@ -404,78 +422,158 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_chol(BigArgs a) {
   double* PART = sm + DTS;         // BIG_NW x 16 partial sums (backward)
   double* YL = PART + BIG_NW * 16; // 16: block right-hand side (backward)
   int* flag = (int*)(YL + 16);
-  double* PC = sm + DTS + BIG_NW * 16 + 16 + 2;  // cached block column, column-major tiles
+  double* LJ = sm + DTS + BIG_NW * 16 + 16 + 2;  // staged L_Jk tiles [jj][kk][256], row-major
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int NT = a.NT;
   if (threadIdx.x == 0) *flag = 0;
-  for (int k = 0; k < NT; ++k) {
-    if (wave == 0) {
-      const double* Akk = H + (size_t)big_tile_index(k, k, NT) * 256;
-      for (int e = lane; e < 256; e += 64) DT[e] = -Akk[e];
-      wave_lds_sync();
-      const bool bad = panel(DT, lane);
-      if (bad && lane == 0) *flag = 1;
-      wave_lds_sync();
-      block_fwd(DT, BV + 16 * k, YV + 16 * k, lane);  // y_k = L_kk^-1 b_k
-      for (int e = lane; e < DTS; e += 64) LTg[(size_t)k * DTS + e] = DT[e];
-    }
-    __syncthreads();
-    if (*flag) break;
-    const bool cached = (NT - 1 - k) <= a.cache_tiles;
-    // TRSM: L_Ik = A_Ik L_kk^-T, I > k; b_I -= L_Ik y_k
-    for (int I = k + 1 + wave; I < NT; I += BIG_NW) {
-      double* Ak = H + (size_t)big_tile_index(I, k, NT) * 256;
-      double av[4], bv[4];
+  for (int k0 = 0; k0 < NT; k0 += BIG_KB) {
+    const int kend = min(k0 + BIG_KB, NT);
+    // ---- panel phase, left-looking inside the block column: at step k every tile
+    // (I, k), I >= k, gets all of its in-block updates in ONE pass (K = 16 (k - k0),
+    // L_kk' operands from LDS), then the TRSM.  Two workgroup barriers per k.
+    // LB (= the LJ region, free until the trailing phase): L_Ik' for k0 <= k' < I < kend.
+    double* LB = LJ;
+    for (int k = k0; k < kend; ++k) {
+      const int nk = k - k0;
+      if (wave == 0) {
+        // diagonal tile: A_kk - sum L_kk' L_kk'^T -> DT (negated), panel, y_k
+        const double* Akk = H + (size_t)big_tile_index(k, k, NT) * 256;
+        d4 c;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        av[r] = Ak[(lane & 15) * 16 + 4 * r + (lane >> 4)];
-        bv[r] = DT[(4 * r + (lane >> 4)) * LIS + (lane & 15)];
-      }
-      d4 u = {0.0, 0.0, 0.0, 0.0};
+        for (int r = 0; r < 4; ++r) c[r] = Akk[64 * r + lane];
+        for (int kk = 0; kk < nk && !(MHE_BIG_KO & 2); ++kk) {
+          const double* Lt = LB + (nk * BIG_KB + kk) * 256;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) u = __builtin_amdgcn_mfma_f64_16x16x4f64(av[r], bv[r], u, 0, 0, 0);
-      const double yc = YV[16 * k + (lane & 15)];
+          for (int r = 0; r < 4; ++r) {
+            const double v = Lt[64 * r + lane];
+            c = __builtin_amdgcn_mfma_f64_16x16x4f64(-v, v, c, 0, 0, 0);
+          }
+        }
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int tr = (lane >> 4) + 4 * r, tc = lane & 15;
-        Ak[tr * 16 + tc] = u[r];
-        if (cached) PC[(size_t)(I - k - 1) * 256 + tc * 16 + tr] = u[r];
-        const double s = row16_sum(u[r] * yc);
-        if ((lane & 15) == r) BV[16 * I + tr] -= s;
-      }
-    }
-    __syncthreads();
-    // trailing update A_IJ -= L_Ik L_Jk^T, k < J <= I
-    const int m = NT - 1 - k;
-    const int npairs = m * (m + 1) / 2;
-    for (int t = wave; t < npairs; t += BIG_NW) {
-      int jj = 0, base = 0;
-      while (t >= base + (m - jj)) {
-        base += m - jj;
-        ++jj;
-      }
-      const int J = k + 1 + jj, I = J + (t - base);
-      double* C = H + (size_t)big_tile_index(I, J, NT) * 256;
-      d4 c;
-      double av[4], bv[4];
+        for (int r = 0; r < 4; ++r) DT[64 * r + lane] = -c[r];
+        wave_lds_sync();
+        const bool bad = panel(DT, lane);
+        if (bad && lane == 0) *flag = 1;
+        wave_lds_sync();
+        block_fwd(DT, BV + 16 * k, YV + 16 * k, lane);  // y_k = L_kk^-1 b_k
+        for (int e = lane; e < DTS; e += 64) LTg[(size_t)k * DTS + e] = DT[e];
+      } else {
+        // rows I > k: c' = A_Ik^T - sum_k' L_kk' L_Ik'^T, stored k-major in place (= A_Ik^T row-major)
+        for (int I = k + wave; I < NT; I += BIG_NW - 1) {
+          double* Ak = H + (size_t)big_tile_index(I, k, NT) * 256;
+          d4 c;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        c[r] = C[((lane >> 4) + 4 * r) * 16 + (lane & 15)];
-        const int kk = 4 * r + (lane >> 4), mm = lane & 15;
-        if (cached) {
-          av[r] = -PC[(size_t)(I - k - 1) * 256 + kk * 16 + mm];
-          bv[r] = PC[(size_t)(J - k - 1) * 256 + kk * 16 + mm];
-        } else {
-          av[r] = -H[(size_t)big_tile_index(I, k, NT) * 256 + mm * 16 + kk];
-          bv[r] = H[(size_t)big_tile_index(J, k, NT) * 256 + mm * 16 + kk];
+          for (int r = 0; r < 4; ++r) c[r] = Ak[(lane & 15) * 16 + 4 * r + (lane >> 4)];
+          for (int kk = 0; kk < nk && !(MHE_BIG_KO & 2); ++kk) {
+            const double* Lk = LB + (nk * BIG_KB + kk) * 256;
+            const double* LI = H + (size_t)big_tile_index(I, k0 + kk, NT) * 256;
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              c = __builtin_amdgcn_mfma_f64_16x16x4f64(-Lk[64 * r + lane], LI[64 * r + lane], c, 0, 0, 0);
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) Ak[64 * r + lane] = c[r];
         }
       }
+      __syncthreads();
+      if (*flag) break;
+      // TRSM: L_Ik^T = L_kk^-1 A_Ik^T (k-major result), b_I -= L_Ik y_k; in-block L_Ik also to LB
+      const double yk = YV[16 * k + (lane >> 4)], yk1 = YV[16 * k + 4 + (lane >> 4)],
+                   yk2 = YV[16 * k + 8 + (lane >> 4)], yk3 = YV[16 * k + 12 + (lane >> 4)];
+      for (int I = k + 1 + wave; I < NT && !(MHE_BIG_KO & 4); I += BIG_NW) {
+        double* Ak = H + (size_t)big_tile_index(I, k, NT) * 256;
+        double av[4], bv[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) c = __builtin_amdgcn_mfma_f64_16x16x4f64(av[r], bv[r], c, 0, 0, 0);
+        for (int r = 0; r < 4; ++r) {
+          av[r] = DT[(4 * r + (lane >> 4)) * LIS + (lane & 15)];  // L_kk^-1 [lane & 15][4r + (lane >> 4)]
+          bv[r] = Ak[64 * r + lane];
+        }
+        d4 u = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-      for (int r = 0; r < 4; ++r) C[((lane >> 4) + 4 * r) * 16 + (lane & 15)] = c[r];
+        for (int r = 0; r < 4; ++r) u = __builtin_amdgcn_mfma_f64_16x16x4f64(av[r], bv[r], u, 0, 0, 0);
+        // u[r] = L_Ik[lane & 15][(lane >> 4) + 4 r]
+        double* LBs = (I < kend) ? LB + ((I - k0) * BIG_KB + nk) * 256 : nullptr;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          Ak[64 * r + lane] = u[r];
+          if (LBs) LBs[64 * r + lane] = u[r];
+        }
+        double s = u[0] * yk + u[1] * yk1 + u[2] * yk2 + u[3] * yk3;
+        s += __shfl_xor(s, 16);
+        s += __shfl_xor(s, 32);
+        if (lane < 16) BV[16 * I + lane] -= s;
+      }
+      __syncthreads();
     }
-    __syncthreads();
+    if (*flag) break;
+    // ---- trailing update with K = (kend - k0) tiles
+    const int kb = kend - k0;
+    for (int J0 = kend; J0 < NT && !(MHE_BIG_KO & 1); J0 += BIG_JB) {
+      const int jb = min(BIG_JB, NT - J0);
+      // stage L_Jk (jb x kb tiles) into LDS
+      for (int e = threadIdx.x; e < jb * kb * 256; e += BIG_NTHREADS) {
+        const int t = e >> 8, jj = t / kb, kk = t % kb;
+        LJ[e] = H[(size_t)big_tile_index(J0 + jj, k0 + kk, NT) * 256 + (e & 255)];
+      }
+      __syncthreads();
+      for (int I = J0 + wave; I < NT; I += BIG_NW) {
+        const int jmax = min(jb, I - J0 + 1);
+        if (jmax == BIG_JB && kb == BIG_KB) {
+          // full row of the slab: BIG_JB accumulators, L_Ik operands streamed (one k tile ahead)
+          d4 c[BIG_JB];
+#pragma unroll
+          for (int jj = 0; jj < BIG_JB; ++jj) {
+            const double* C = H + (size_t)big_tile_index(I, J0 + jj, NT) * 256;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) c[jj][r] = C[64 * r + lane];
+          }
+          const double* LI0 = H + (size_t)big_tile_index(I, k0, NT) * 256;
+          double av[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) av[r] = -LI0[64 * r + lane];
+#pragma unroll 1
+          for (int kk = 0; kk < BIG_KB; ++kk) {
+            double an[4];
+            const double* LIn = H + (size_t)big_tile_index(I, k0 + min(kk + 1, BIG_KB - 1), NT) * 256;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) an[r] = -LIn[64 * r + lane];
+#pragma unroll
+            for (int jj = 0; jj < BIG_JB; ++jj) {
+              const double* Bt = LJ + (jj * BIG_KB + kk) * 256;
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                c[jj] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[r], Bt[64 * r + lane], c[jj], 0, 0, 0);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) av[r] = an[r];
+          }
+#pragma unroll
+          for (int jj = 0; jj < BIG_JB; ++jj) {
+            double* C = H + (size_t)big_tile_index(I, J0 + jj, NT) * 256;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) C[64 * r + lane] = c[jj][r];
+          }
+        } else {
+          // edge rows / last slab / short block: one tile at a time
+          for (int jj = 0; jj < jmax; ++jj) {
+            double* C = H + (size_t)big_tile_index(I, J0 + jj, NT) * 256;
+            d4 c;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) c[r] = C[64 * r + lane];
+            for (int kk = 0; kk < kb; ++kk) {
+              const double* LI = H + (size_t)big_tile_index(I, k0 + kk, NT) * 256;
+              const double* Bt = LJ + (jj * kb + kk) * 256;
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                c = __builtin_amdgcn_mfma_f64_16x16x4f64(-LI[64 * r + lane], Bt[64 * r + lane], c, 0, 0, 0);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) C[64 * r + lane] = c[r];
+          }
+        }
+      }
+      __syncthreads();
+    }
   }
   if (*flag) {
     if (threadIdx.x == 0) a.state[b] = MHE_STATUS_NOT_SPD;
@@ -489,7 +587,7 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_chol(BigArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int tr = (lane >> 4) + 4 * r;
-        pv += L[tr * 16 + (lane & 15)] * YV[16 * I + tr];
+        pv += L[(lane & 15) * 16 + tr] * YV[16 * I + tr];  // L_Ik[tr][lane & 15], k-major tile
       }
     }
     pv += __shfl_xor(pv, 16);
@@ -597,7 +695,7 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_border(BigArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           c[r] = Zp[(size_t)ii * dp + 16 * I + mg + 4 * r];
-          av[r] = -L[ii * 16 + 4 * r + mg];
+          av[r] = -L[(4 * r + mg) * 16 + ii];  // L_Ik[i][m], k-major tile
           bv[r] = zload(k, r);
         }
 #pragma unroll
@@ -629,7 +727,7 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_border(BigArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           c[r] = Zp[(size_t)ii * dp + 16 * J + mg + 4 * r];
-          av[r] = -L[(4 * r + mg) * 16 + ii];  // (L_kJ^T)[i][m] = L_kJ[m][i]
+          av[r] = -L[ii * 16 + 4 * r + mg];  // (L_kJ^T)[i][m] = L_kJ[m][i], k-major tile
           bv[r] = zload(k, r);
         }
 #pragma unroll

@@ -1465,13 +1465,7 @@ struct LaunchBig {
   int run() {
     BigArgs& A = *a;
     const int ntiles = A.NT * (A.NT + 1) / 2;
-    const size_t fixed = (size_t)(DTS + BIG_NW * 16 + 16 + 2) * sizeof(double);
-    const size_t lds_max = 160 * 1024 - 1024;
-    int cache = (int)((lds_max - fixed) / (256 * sizeof(double)));
-    if (cache > A.NT - 1) cache = A.NT - 1;
-    if (cache < 0) cache = 0;
-    A.cache_tiles = cache;
-    const int smem = (int)(fixed + (size_t)cache * 256 * sizeof(double));
+    const int smem = BIG_CHOL_LDS * (int)sizeof(double);
     if (hipFuncSetAttribute((const void*)k_big_chol, hipFuncAttributeMaxDynamicSharedMemorySize, smem) != hipSuccess)
       return MHE_ERR_HIP;
     if (hipMemcpyAsync(A.X, X0, sizeof(double) * batch * A.P * A.n, hipMemcpyDeviceToDevice, st) != hipSuccess)
