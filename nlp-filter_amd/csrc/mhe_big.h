@@ -327,10 +327,27 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_resid(BigArgs a, int final
 }
 
 // ------------------------------------------------------------ assembly
-// One wave per tile; grid (tiles / 4 per block, B).
+// Block (a, b) of H (component-major) is the P x P matrix
+//   a^2 Qw_ab (D^T C D) - a (D^T diag(E_ab) + diag(E_ba) D) + diag(FtE_ab)
+//   + M_ab,   M_ab = Phi_E^T diag(G_ab) Phi_E   (G_e = sum_{i in e} H_i^T R_i H_i)
+// M_ab is a GEMM over the E epochs, symmetric (M_ab = M_ab^T = M_ba), and all
+// component pairs share the same operands Phi_E: one wave takes one tile position
+// (it >= jt) and a chunk of up to 8 pairs (ca >= cb) -- one MFMA accumulator per
+// pair -- so each K step of 4 epochs loads 2 Phi_E values (L2-resident, shared by
+// every trajectory) and feeds up to 8 MFMAs (G_e[ca][cb] read per lane; 8 accumulators keep ~4 waves/SIMD).  The
+// dynamics terms are added elementwise at the write; an off-diagonal pair also
+// writes the transposed tile (jt, it) from the same accumulator.
+template <int n>
+struct BigPairs {
+  static constexpr int NPR = n * (n + 1) / 2;
+  static constexpr int NCH = (NPR + 7) / 8;
+  static constexpr int PCH = (NPR + NCH - 1) / NCH;
+};
+
 template <class DYN, class MEAS>
-__global__ __launch_bounds__(256) void k_big_assemble(BigArgs a) {
+__global__ __launch_bounds__(256, 4) void k_big_assemble(BigArgs a) {
   constexpr int n = DYN::n, p = MEAS::p;
+  constexpr int NPR = BigPairs<n>::NPR, NCH = BigPairs<n>::NCH, PCH = BigPairs<n>::PCH;
   const int b = blockIdx.y;
   if (a.state[b] != BIG_RUNNING) return;
   const BigConst CL = big_const_layout(a.P, a.M, n, p, a.nc);
@@ -343,48 +360,90 @@ __global__ __launch_bounds__(256) void k_big_assemble(BigArgs a) {
   const double* Pw = (const double*)(a.cbuf + CL.Pw);
   const double* PhiE = (const double*)(a.cbuf + CL.PhiE);
   const int E = a.M > 0 ? *(const int*)(a.cbuf + CL.ne) : 0;
-  const int lane = threadIdx.x & 63;
-  const int ntiles = a.NT * (a.NT + 1) / 2;
-  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (t >= ntiles) return;
-  int J = 0, base = 0;
-  while (t >= base + (a.NT - J)) {
-    base += a.NT - J;
-    ++J;
+  const int E4 = (E + 3) & ~3;  // K steps of 4 epochs (av = bv = 0 past E)
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int NTc = a.NTc, P = a.P;
+  const int npos = NTc * (NTc + 1) / 2;
+  const int u = blockIdx.x * 4 + wave;
+  if (u >= npos * NCH) return;
+  const int ch = u % NCH;
+  int it = 0, pos = u / NCH;  // pos -> (it, jt), jt <= it
+  while (pos > it) {
+    pos -= it + 1;
+    ++it;
   }
-  const int I = J + (t - base);
-  const int ca = I / a.NTc, it = I % a.NTc, cb = J / a.NTc, jt = J % a.NTc;
-  // measurement part: sum_e Phi_E[e][j] G_e[ca][cb] Phi_E[e][l], MFMA over epochs
-  d4 acc = {0.0, 0.0, 0.0, 0.0};
-  {
-    const int jr = 16 * it + (lane & 15), lc = 16 * jt + (lane & 15);
-    for (int e0 = 0; e0 < E; e0 += 4) {
-      const int e = e0 + (lane >> 4);
-      double av = 0.0, bv = 0.0;
-      if (e < E) {
-        const double g = ws[WL.Ge + (size_t)e * n * n + ca * n + cb];
-        av = jr < a.P ? PhiE[(size_t)e * a.P + jr] * g : 0.0;
-        bv = lc < a.P ? PhiE[(size_t)e * a.P + lc] : 0.0;
-      }
-      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
-    }
-  }
-  double* tile = H + (size_t)t * 256;
+  const int jt = pos;
+  d4 acc[PCH];
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int tr = (lane >> 4) + 4 * r, tc = lane & 15;
-    const int j = 16 * it + tr, l = 16 * jt + tc;
-    double v;
-    if (j < a.P && l < a.P) {
-      v = acc[r] + a.alpha * a.alpha * Qw[ca * n + cb] * DCD[(size_t)j * a.P + l] -
-          a.alpha * (D[(size_t)l * a.P + j] * ws[WL.Es + (l * n + ca) * n + cb] +
-                     D[(size_t)j * a.P + l] * ws[WL.Es + (j * n + cb) * n + ca]);
-      if (j == l) v += ws[WL.FtE + (j * n + ca) * n + cb];
-      if (a.has_prior && j == 0 && l == 0) v += Pw[ca * n + cb];
-    } else {
-      v = (I == J && tr == tc) ? 1.0 : 0.0;
+  for (int q = 0; q < PCH; ++q) acc[q] = d4{0.0, 0.0, 0.0, 0.0};
+  const int row = 16 * it + (lane & 15), col = 16 * jt + (lane & 15);
+  const bool vr = row < P, vc = col < P;
+  const int p0 = ch * PCH;
+  int ca = 0, cb = p0;  // first pair of the chunk
+  while (cb > ca) {
+    cb -= ca + 1;
+    ++ca;
+  }
+  int goff[PCH];        // offsets of G_e[ca][cb] for the chunk's pairs
+  {
+    int x = ca, y = cb;
+#pragma unroll
+    for (int q = 0; q < PCH; ++q) {
+      goff[q] = x * n + y;
+      if (++y > x) {
+        y = 0;
+        ++x;
+      }
     }
-    tile[tr * 16 + tc] = v;
+  }
+  const double* Ge = ws + WL.Ge;
+  for (int e0 = 0; e0 < E4; e0 += 4) {
+    const int e = e0 + (lane >> 4);
+    double av = 0.0, bv = 0.0;
+    const int ec = e < E ? e : E - 1;
+    if (e < E) {
+      av = vr ? PhiE[(size_t)e * P + row] : 0.0;
+      bv = vc ? PhiE[(size_t)e * P + col] : 0.0;
+    }
+    const double* gp = Ge + (size_t)ec * n * n;
+#pragma unroll
+    for (int q = 0; q < PCH; ++q)
+      if (p0 + q < NPR) acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av * gp[goff[q]], bv, acc[q], 0, 0, 0);
+  }
+#pragma unroll
+  for (int q = 0; q < PCH; ++q) {
+    if (p0 + q < NPR) {
+      const double qab = a.alpha * a.alpha * Qw[ca * n + cb];
+      // tile (it, jt) of block (ca, cb) and, off the diagonal pair, its transpose into (jt, it)
+#pragma unroll
+      for (int tp = 0; tp < 2; ++tp) {
+        if (tp == 1 && (ca == cb || it == jt)) break;
+        const int ti = tp ? jt : it, tj = tp ? it : jt;
+        const int I = ca * NTc + ti, J = cb * NTc + tj;
+        double* tile = H + (size_t)big_tile_index(I, J, a.NT) * 256;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int cr = (lane >> 4) + 4 * r, cc = lane & 15;  // accumulator element (cr, cc) of tile (it, jt)
+          const int tr = tp ? cc : cr, tc = tp ? cr : cc;       // position in the written tile
+          const int j = 16 * ti + tr, l = 16 * tj + tc;
+          double v;
+          if (j < P && l < P) {
+            v = acc[q][r] + qab * DCD[(size_t)j * P + l] -
+                a.alpha * (D[(size_t)l * P + j] * ws[WL.Es + (l * n + ca) * n + cb] +
+                           D[(size_t)j * P + l] * ws[WL.Es + (j * n + cb) * n + ca]);
+            if (j == l) v += ws[WL.FtE + (j * n + ca) * n + cb];
+            if (a.has_prior && j == 0 && l == 0) v += Pw[ca * n + cb];
+          } else {
+            v = (I == J && tr == tc) ? 1.0 : 0.0;
+          }
+          tile[tr * 16 + tc] = v;
+        }
+      }
+    }
+    if (++cb > ca) {
+      cb = 0;
+      ++ca;
+    }
   }
 }
 

@@ -1464,7 +1464,7 @@ struct LaunchBig {
   template <class DYN, class MEAS>
   int run() {
     BigArgs& A = *a;
-    const int ntiles = A.NT * (A.NT + 1) / 2;
+    const int npos = A.NTc * (A.NTc + 1) / 2;
     const int smem = BIG_CHOL_LDS * (int)sizeof(double);
     if (hipFuncSetAttribute((const void*)k_big_chol, hipFuncAttributeMaxDynamicSharedMemorySize, smem) != hipSuccess)
       return MHE_ERR_HIP;
@@ -1481,7 +1481,8 @@ struct LaunchBig {
     hipLaunchKernelGGL(k_big_init, dim3((batch + 255) / 256), dim3(256), 0, st, batch, A.state, A.iters);
     for (int it = 0; it < max_iter; ++it) {
       hipLaunchKernelGGL((k_big_resid<DYN, MEAS>), dim3(batch), dim3(BIG_NTHREADS), 0, st, A, 0);
-      hipLaunchKernelGGL((k_big_assemble<DYN, MEAS>), dim3((ntiles + 3) / 4, batch), dim3(256), 0, st, A);
+      hipLaunchKernelGGL((k_big_assemble<DYN, MEAS>), dim3((npos * BigPairs<DYN::n>::NCH + 3) / 4, batch), dim3(256), 0,
+                         st, A);
       hipLaunchKernelGGL(k_big_chol, dim3(batch), dim3(BIG_NTHREADS), smem, st, A);
       if (K > 0) hipLaunchKernelGGL((k_big_border<DYN::n, MEAS::p>), dim3(batch), dim3(BIG_NTHREADS), smem_b, st, A);
       hipLaunchKernelGGL((k_big_update<DYN::n>), dim3(batch), dim3(256), 0, st, A);
