@@ -461,13 +461,15 @@ __global__ __launch_bounds__(256, 4) void k_big_assemble(BigArgs a) {
 //                 all waves); each wave walks tile rows I, holds L_I (A operands)
 //                 in registers and updates the row's (up to) four tiles.
 constexpr int BIG_KB = 8;      // tile columns per super-block
-constexpr int BIG_JB = 8;      // tile columns per LDS-staged trailing slab
+constexpr int BIG_JB = 4;      // tile columns per LDS-staged trailing slab
 #ifndef MHE_BIG_KO
 #define MHE_BIG_KO 0  // knock-out mask for timing probes only (tools/ko_big.sh): 1 trailing, 2 in-block, 4 TRSM
 #endif
-constexpr int BIG_CHOL_LDS = DTS + BIG_NW * 16 + 16 + 2 + BIG_JB * BIG_KB * 256;  // doubles
+constexpr int BIG_LB_TILES = BIG_KB * (BIG_KB - 1) / 2;
+constexpr int BIG_SLAB_TILES = BIG_JB * BIG_KB > BIG_LB_TILES ? BIG_JB * BIG_KB : BIG_LB_TILES;
+constexpr int BIG_CHOL_LDS = DTS + BIG_NW * 16 + 16 + 2 + BIG_SLAB_TILES * 256;  // doubles
 
-__global__ __launch_bounds__(BIG_NTHREADS) void k_big_chol(BigArgs a) {
+__global__ __launch_bounds__(BIG_NTHREADS, 4) void k_big_chol(BigArgs a) {
   const int b = blockIdx.x;
   if (a.state[b] != BIG_RUNNING) return;
   const BigWs WL = big_ws_layout(a.P, a.M, a.n, a.NT, a.nz, a.nc);
@@ -490,7 +492,8 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_chol(BigArgs a) {
     // ---- panel phase, left-looking inside the block column: at step k every tile
     // (I, k), I >= k, gets all of its in-block updates in ONE pass (K = 16 (k - k0),
     // L_kk' operands from LDS), then the TRSM.  Two workgroup barriers per k.
-    // LB (= the LJ region, free until the trailing phase): L_Ik' for k0 <= k' < I < kend.
+    // LB (= the LJ region, free until the trailing phase): L_Ik' for k0 <= k' < I < kend, packed
+    // strictly-lower: slot (I - k0)(I - k0 - 1)/2 + (k' - k0).
     double* LB = LJ;
     for (int k = k0; k < kend; ++k) {
       const int nk = k - k0;
@@ -501,7 +504,7 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_chol(BigArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) c[r] = Akk[64 * r + lane];
         for (int kk = 0; kk < nk && !(MHE_BIG_KO & 2); ++kk) {
-          const double* Lt = LB + (nk * BIG_KB + kk) * 256;
+          const double* Lt = LB + (nk * (nk - 1) / 2 + kk) * 256;
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const double v = Lt[64 * r + lane];
@@ -524,7 +527,7 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_chol(BigArgs a) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) c[r] = Ak[(lane & 15) * 16 + 4 * r + (lane >> 4)];
           for (int kk = 0; kk < nk && !(MHE_BIG_KO & 2); ++kk) {
-            const double* Lk = LB + (nk * BIG_KB + kk) * 256;
+            const double* Lk = LB + (nk * (nk - 1) / 2 + kk) * 256;
             const double* LI = H + (size_t)big_tile_index(I, k0 + kk, NT) * 256;
 #pragma unroll
             for (int r = 0; r < 4; ++r)
@@ -551,7 +554,7 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_chol(BigArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) u = __builtin_amdgcn_mfma_f64_16x16x4f64(av[r], bv[r], u, 0, 0, 0);
         // u[r] = L_Ik[lane & 15][(lane >> 4) + 4 r]
-        double* LBs = (I < kend) ? LB + ((I - k0) * BIG_KB + nk) * 256 : nullptr;
+        double* LBs = (I < kend) ? LB + ((I - k0) * (I - k0 - 1) / 2 + nk) * 256 : nullptr;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           Ak[64 * r + lane] = u[r];
