@@ -10,6 +10,15 @@ C2  van_der_pol:       n=2, m=1 (u = 0), full_state, N=100, T=10, M=101, B=1024
     (van_der_pol.py:10,33 scales; R, Q from estimation_example.py:20,33)
 C3  gnss_stationary:   n=5, m=3, pseudorange, N=200, T=200, 201 epochs x 12 sats, B=4096
     (large-system path: d = 1005)
+C4  rc-car:            kinematic_bycicle_and_bias (n=6, m=2) + pseudorange, N=500, T=500,
+    501 epochs x 12 sats, B=8192 over 8 GPUs (d = 3006; rc-car.py:46-47,89-113 at N=500)
+C5  multi-receiver:    multi_receiver (n=8, m=0) + pseudorange + pseudorange_rate per
+    satellite and a 2-D range to the extra variable XA (n_extra=3) per epoch -- mixed
+    rows, N=200, T=200, 201 epochs x (12 + 12 + 1) rows, B=16384 over 8 GPUs
+    (multi-receiver.py:62-100 at N=200; d = 1608 + 3).  BASELINE.json calls it an
+    "N-receiver joint state (~4N dims, N=8)": the reference's own multi-receiver
+    problem has the 8-dim state of receiver B plus receiver A's position XA, and
+    that is the structure used here.
 """
 import numpy as np
 from scipy.interpolate import interp1d
@@ -148,3 +157,119 @@ def make_c3(B=4096, seed=2, N=200):
 
 
 CONFIGS = {"C1": make_c1, "C2": make_c2, "C3": make_c3}
+
+
+def _sky(rng, n_sat, r=2.2e7):
+    az = rng.uniform(0, 2 * np.pi, n_sat)
+    el = rng.uniform(0.3, 1.3, n_sat)
+    return r * np.stack([np.cos(el) * np.cos(az), np.cos(el) * np.sin(az), np.sin(el)], axis=1)
+
+
+def bicycle_rhs(x, u):
+    """dynamics.kinematic_bycicle_and_bias (nlp/dynamics.py:117-136), batch form;
+    x[2] is used as the heading exactly as the reference does."""
+    L = 0.28
+    v = 8.72649116358 * u[:, 0] - 0.856053299155
+    delta = np.deg2rad(28) * u[:, 1]
+    return np.stack([v * np.cos(x[:, 2]), v * np.sin(x[:, 2]), np.zeros_like(v), x[:, 4], np.zeros_like(v),
+                     (v / L) * np.tan(delta)], axis=1)
+
+
+def make_c4(B=1024, seed=3, N=500, epochs=None, n_sat=12):
+    """C4 rc-car shape: bicycle + pseudorange, N=500 (d = 3006).  Synthetic controls
+    (throttle ~0.3, smooth steering) per trajectory, RK4 truth, r_pr and Q as
+    rc-car.py:46-47; 12 satellite slots fixed over the window."""
+    T = float(N)
+    epochs = N + 1 if epochs is None else epochs
+    rng = np.random.default_rng(seed)
+    t_ep = np.linspace(0, T, epochs)
+    sat = _sky(rng, n_sat)
+    ph = rng.uniform(0, 2 * np.pi, (B, 2))
+    th0 = rng.uniform(0.25, 0.35, (B, 1))
+
+    def ctrl(t):
+        t = np.atleast_1d(t)
+        return np.stack([th0 + 0.03 * np.sin(2 * np.pi * t[None, :] / 47.0 + ph[:, :1]),
+                         0.4 * np.sin(2 * np.pi * t[None, :] / 61.0 + ph[:, 1:])], axis=-1)  # (B, len t, 2)
+
+    x0 = np.zeros((B, 6))
+    x0[:, :2] = rng.normal(size=(B, 2)) * 10.0
+    x0[:, 2] = rng.uniform(-np.pi, np.pi, B)
+    x0[:, 3] = rng.normal(size=B) * 100.0
+    x0[:, 4] = rng.normal(size=B) * 0.5
+    xt = _rk4(lambda tt, x: bicycle_rhs(x, ctrl(tt)[:, 0]), x0, t_ep, substeps=4)
+    r_pr = 10.0
+    rho = np.linalg.norm(xt[:, :, None, :3] - sat[None, None], axis=-1) + xt[:, :, None, 3]
+    M = epochs * n_sat
+    Y = (rho + rng.normal(size=rho.shape) * np.sqrt(r_pr)).reshape(B, M, 1)
+    cpm = ChebyshevPseudospectralMethod(N, 0, T)
+    t_nodes = cpm.tau2t(cpm.tau)
+    U = ctrl(t_nodes)
+    X_init = interp1d(t_ep, xt, axis=1)(t_nodes) + rng.normal(size=(B, 1, 6)) * np.array([2.0, 2.0, 0.02, 2.0, 0.05, 0.1])
+    Q = np.diag([1, 1, 0.001, .01, .01, 1])
+    return Workload(name="C4_rc_car", N=N, T=T, n=6, m=2, p=1, M=M, B=B,
+                    dyn="kinematic_bycicle_and_bias", meas="pseudorange", meas_static={"idx": [0, 1, 2, 3]},
+                    t_meas=np.repeat(t_ep, n_sat), Y=Y, U=U, PAR=np.tile(sat, (epochs, 1))[None],
+                    Qw=np.linalg.inv(Q), Rw=np.full((M, 1, 1), 1.0 / r_pr), Pw=None, x0=None,
+                    X_init=X_init, X_true=xt, cpm=cpm)
+
+
+def make_c5(B=2048, seed=4, N=200, epochs=None, n_sat=12):
+    """C5 multi-receiver shape: multi_receiver dynamics (x = [p, b, v, alpha], n=8, m=0),
+    per epoch 12 pseudoranges + 12 pseudorange rates (sat_pos, sat_vel) and one 2-D range
+    to XA (extra decision variable, 3 components; multi-receiver.py:73,99), mixed rows
+    (include/mhe.h).  Weights as multi-receiver.py:77-88 (the script passes inv(Q))."""
+    T = float(N)
+    epochs = N + 1 if epochs is None else epochs
+    rng = np.random.default_rng(seed)
+    t_ep = np.linspace(0, T, epochs)
+    sat0 = _sky(rng, n_sat)
+    svel = rng.normal(size=(n_sat, 3))
+    svel = 3000.0 * svel / np.linalg.norm(svel, axis=1, keepdims=True)
+    p0 = rng.normal(size=(B, 3)) * 10.0
+    hd = rng.uniform(0, 2 * np.pi, B)
+    vel = np.stack([np.cos(hd), np.sin(hd), np.zeros(B)], axis=1) * rng.uniform(0.5, 1.5, (B, 1))
+    b0 = rng.normal(size=B) * 100.0
+    al = rng.normal(size=B) * 0.5
+    # receiver A (truth of XA) 2.4384 m (multi-receiver.py:98) beside the middle of B's track
+    side = np.stack([-np.sin(hd), np.cos(hd), np.zeros(B)], axis=1)
+    xa = p0 + vel * (T / 2) + 2.4384 * side + np.concatenate([np.zeros((B, 2)), rng.normal(size=(B, 1))], 1)
+    r_pr, r_prr, r_range = 100.0, 0.1, 0.01
+    rows, t_rows, Rw = [], [], []
+    Yl = []
+    for k, tk in enumerate(t_ep):
+        sp = sat0 + svel * tk
+        pos = p0 + vel * tk
+        bias = b0 + al * tk
+        for j in range(n_sat):
+            d = pos - sp[j]
+            rho = np.linalg.norm(d, axis=1)
+            rows.append([1, 0, 1, 2, 3, -1, -1, -1] + list(sp[j]) + [0.0, 0.0, 0.0])
+            t_rows.append(tk); Rw.append(1.0 / r_pr)
+            Yl.append(rho + bias + rng.normal(size=B) * np.sqrt(r_pr))
+            los = -d / rho[:, None]
+            rows.append([2, 0, 1, 2, 4, 5, 6, 7] + list(sp[j]) + list(svel[j]))
+            t_rows.append(tk); Rw.append(1.0 / r_prr)
+            Yl.append(np.sum((svel[j][None] - vel) * los, axis=1) + al + rng.normal(size=B) * np.sqrt(r_prr))
+        rows.append([3, 0, 1, 8, 9, -1, -1, -1, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0])
+        t_rows.append(tk); Rw.append(1.0 / r_range)
+        Yl.append(np.sqrt(np.sum((pos[:, :2] - xa[:, :2]) ** 2, axis=1) + 1e-6) + rng.normal(size=B) * np.sqrt(r_range))
+    M = len(rows)
+    cpm = ChebyshevPseudospectralMethod(N, 0, T)
+    t_nodes = cpm.tau2t(cpm.tau)
+    xt = np.zeros((B, t_nodes.shape[0], 8))
+    xt[:, :, :3] = p0[:, None] + vel[:, None] * t_nodes[None, :, None]
+    xt[:, :, 3] = b0[:, None] + al[:, None] * t_nodes[None]
+    xt[:, :, 4:7] = vel[:, None]
+    xt[:, :, 7] = al[:, None]
+    X_init = xt + rng.normal(size=(B, 1, 8)) * np.array([2.0, 2.0, 2.0, 2.0, 0.05, 0.05, 0.05, 0.05])
+    Q = np.diag([0.01, 0.01, 0.01, 0.01, 1., 1., 0.01, 0.01])
+    return Workload(name="C5_multi_receiver", N=N, T=T, n=8, m=0, p=1, M=M, B=B,
+                    dyn="multi_receiver", meas="mixed", meas_static={}, n_extra=3,
+                    t_meas=np.asarray(t_rows), Y=np.stack(Yl, axis=1)[:, :, None], U=None,
+                    PAR=np.asarray(rows, dtype=np.float64)[None], Qw=np.linalg.inv(Q), Rw=np.asarray(Rw),
+                    Pw=None, x0=None, X_init=X_init, Z_init=xa + rng.normal(size=(B, 3)) * 0.5,
+                    X_true=xt, Z_true=xa, cpm=cpm)
+
+
+CONFIGS.update({"C4": make_c4, "C5": make_c5})

@@ -242,5 +242,6 @@ class BatchSolver:
 def from_workload(w, device="cuda", **kw):
     """BatchSolver for a mhe.configs.Workload (kw: dyn_cost, huber_delta, bounds)."""
     Phi = w.cpm.lagrange_matrix(w.t_meas)
+    kw.setdefault("n_extra", getattr(w, "n_extra", 0))
     return BatchSolver(w.N, w.T, w.dyn, w.meas, w.cpm.D, (w.T / 2.0) * w.cpm.w, Phi, w.Qw, w.Rw,
                        Pw=w.Pw, meas_idx=w.meas_static.get("idx"), device=device, **kw)

@@ -86,6 +86,20 @@ def masked_rows(Rw):
     return np.all(Rw.reshape(Rw.shape[:2] + (int(np.prod(Rw.shape[2:])),)) == 0.0, axis=-1)
 
 
+def _meas_block(Phi, G):
+    """sum_i Phi_ij Phi_il G_i[a, c] -> (B, P, n, P, n).  Rows with bitwise-equal Phi rows
+    (one measurement epoch) are summed first -- the same sum, regrouped -- so the
+    contraction is E x P^2 n^2 instead of M x P^2 n^2 (C4: 501 instead of 6012)."""
+    B, M, n, _ = G.shape
+    P = Phi.shape[1]
+    uq, inv = np.unique(Phi, axis=0, return_inverse=True)
+    Ge = np.zeros((B, uq.shape[0], n, n))
+    np.add.at(Ge, (slice(None), inv.ravel()), G)
+    A = (uq[:, :, None] * Ge.reshape(B, uq.shape[0], 1, n * n)[:, :, :, :])     # (B, E, P, n*n)
+    out = np.einsum("bejq,el->bjlq", A, uq, optimize=True).reshape(B, P, P, n, n)
+    return out.transpose(0, 1, 3, 2, 4)
+
+
 def normal_equations(pb, X, U, Y, PAR=None, x0=None):
     """Structured GN normal equations. Returns H (B,d,d), g (B,d), cost (B,)."""
     X = np.asarray(X, dtype=np.float64)
@@ -118,7 +132,7 @@ def normal_equations(pb, X, U, Y, PAR=None, x0=None):
     Rw = pb.Rw if pb.Rw.ndim == 4 else np.broadcast_to(pb.Rw[None], (B,) + pb.Rw.shape)
     Hm = np.where(masked_rows(Rw)[..., None, None], 0.0, Hm)
     G = np.einsum("zipa,zipq,ziqc->ziac", Hm, Rw, Hm)              # (B,M,n,n)
-    H4 += np.einsum("ij,il,ziac->zjalc", pb.Phi, pb.Phi, G)
+    H4 += _meas_block(pb.Phi, G)
     ge = np.einsum("zipa,zipq,ziq->zia", Hm, Rw, e)
     g -= np.einsum("ij,zia->zja", pb.Phi, ge)
     if pb.Pw is not None:
