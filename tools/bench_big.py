@@ -1,22 +1,53 @@
-"""Large-system path timing (C3 shape): GN collocation-point updates/s at batch B (tools only).
-    python tools/bench_big.py [B] [iters]"""
-import os, sys, time
+"""Large-system path timing (tools only): C3 / C4 / C5 shapes of BASELINE.json.
+
+    python tools/bench_big.py [C3|C4|C5] [B] [iters]
+
+GN collocation-point updates/s = B * P * iters / device time (HIP events around one
+mhe_gn_solve_ws call with tol = 0, inputs resident), and the algorithmic FP64 rate
+by SURVEY.md §8(d)'s count per trajectory-iteration:
+    F = d^3/3 + 2 d^2 + E P^2 nnz(G_e) + 2 P^2 n^2 + 4 P n^3
+(nnz(G_e): state components the epoch's rows touch, squared).
+"""
+import json
+import os
+import sys
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "nlp-filter_amd"))
+import numpy as np  # noqa: E402
 import torch  # noqa: E402
 from mhe import configs, solver  # noqa: E402
-B = int(sys.argv[1]) if len(sys.argv) > 1 else 256
-it = int(sys.argv[2]) if len(sys.argv) > 2 else 3
-w = configs.make_c3(B=B)
+
+cfg = sys.argv[1] if len(sys.argv) > 1 else "C3"
+B = int(sys.argv[2]) if len(sys.argv) > 2 else 256
+it = int(sys.argv[3]) if len(sys.argv) > 3 else 3
+w = configs.CONFIGS[cfg](B=B)
 s = solver.from_workload(w)
-st = s.prepare(w.X_init, w.U, w.Y, w.PAR)
-outs = (torch.empty_like(st[0]), torch.empty(B, dtype=torch.float64, device="cuda"),
-        torch.empty(B, dtype=torch.int32, device="cuda"), torch.empty(B, dtype=torch.int32, device="cuda"))
-s.solve_staged(st, outs, 1, 0.0)
+P, n = w.P, w.n
+d = P * n
+E = np.unique(w.t_meas).shape[0]
+touched = {"C2": 2, "C3": 4, "C4": 4, "C5": 8}[cfg]
+F = d ** 3 / 3 + 2 * d * d + E * P * P * touched ** 2 + 2 * P * P * n * n + 4 * P * n ** 3
+Z0 = getattr(w, "Z_init", None)
+
+
+def run(k):
+    return s.solve(w.X_init, w.U, w.Y, w.PAR, max_iter=k, tol=0.0, Z0=Z0)
+
+
+run(1)
 torch.cuda.synchronize()
-t0 = time.perf_counter()
-s.solve_staged(st, outs, it, 0.0)
-torch.cuda.synchronize()
-dt = time.perf_counter() - t0
-print(f"C3 large-system path B={B} iters={it}: {dt * 1e3:.1f} ms, {B * w.P * it / dt:.3e} pt-updates/s, "
-      f"workspace {s.lib.mhe_workspace_bytes(s.dims, B) / 2**30:.2f} GiB, status {outs[3].cpu().unique().tolist()}")
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+# inputs are staged inside solve() before the first launch; time the GN launches only
+# by differencing an iters-long and a 1-iteration solve (same staging, same epilogue)
+e0.record(); run(1); e1.record(); torch.cuda.synchronize(); t1 = e0.elapsed_time(e1)
+e0.record(); out = run(it + 1); e1.record(); torch.cuda.synchronize(); tk = e0.elapsed_time(e1)
+dt = (tk - t1) / 1e3
+st = out[3].cpu().numpy()
+res = {"config": cfg, "workload": w.name, "B": B, "iters": it, "d": d, "P": P, "n": n, "E": int(E),
+       "ms_per_iter": dt / it * 1e3, "pt_updates_per_s": B * P * it / dt,
+       "mflop_per_traj_iter": F / 1e6, "achieved_tflops": F * B * it / dt / 1e12,
+       "frac_fp64_peak": F * B * it / dt / 1e12 / 78.6,
+       "workspace_gib": s.lib.mhe_workspace_bytes(s.dims, B) / 2 ** 30,
+       "status": sorted(set(st.tolist()))}
+print(json.dumps(res))
