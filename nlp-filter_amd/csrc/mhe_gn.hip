@@ -723,9 +723,15 @@ __device__ __forceinline__ bool panel(double* DTk, int lane) {
 #pragma unroll
   for (int c = 0; c < 16; c += 2) {
     const double2 a2 = *(const double2*)(DTk + i * 16 + c);
-    v[c] = erow ? (c == i ? 1.0 : 0.0) : -a2.x;  // DT holds -A_kk
-    v[c + 1] = erow ? (c + 1 == i ? 1.0 : 0.0) : -a2.y;
+    v[c] = a2.x;
+    v[c + 1] = a2.y;
   }
+  // materialise the loads in every lane before the select (otherwise the loads are
+  // sunk into 16 exec-masked branches)
+#pragma unroll
+  for (int c = 0; c < 16; ++c) asm volatile("" : "+v"(v[c]));
+#pragma unroll
+  for (int c = 0; c < 16; ++c) v[c] = erow ? (c == i ? 1.0 : 0.0) : -v[c];  // DT holds -A_kk
   bool bad = false;
 #pragma unroll
   for (int c = 0; c < 16; ++c) {
