@@ -294,10 +294,11 @@ __device__ __forceinline__ void dot_rows_part(const double* __restrict__ Mt, int
 #pragma unroll
     for (int c = 0; c < n; ++c) acc[c] += mv * Xs[j * n + c];
   }
+  static_assert(TPR == 4, "quad reductions below assume 4 lanes per row");
 #pragma unroll
-  for (int o = 1; o < TPR; o <<= 1)
+  for (int c = 0; c < n; ++c) acc[c] += dpp_d<0xB1>(acc[c]);  // lane ^ 1 (DPP: no bpermute address registers)
 #pragma unroll
-    for (int c = 0; c < n; ++c) acc[c] += __shfl_xor(acc[c], o);
+  for (int c = 0; c < n; ++c) acc[c] += dpp_d<0x4E>(acc[c]);  // lane ^ 2
 }
 
 // Per-node dynamics quantities (nlp/nlp.py:225-245):
@@ -517,13 +518,12 @@ __device__ __forceinline__ double grad_phase(const GnArgs& a, const ConstLayout&
 #pragma unroll
       for (int c = 0; c < n; ++c) s[c] += mv * vec[k * n + c];
     }
+    static_assert(HP == 2, "quad DPP reductions below assume TPR == 4");
 #pragma unroll
-    for (int o2 = 1; o2 < HP; o2 <<= 1)
-#pragma unroll
-      for (int c = 0; c < n; ++c) s[c] += __shfl_xor(s[c], o2);
+    for (int c = 0; c < n; ++c) s[c] += dpp_d<0xB1>(s[c]);  // lane ^ 1
     double o[n];
 #pragma unroll
-    for (int c = 0; c < n; ++c) o[c] = __shfl_xor(s[c], HP);  // the other column's sum
+    for (int c = 0; c < n; ++c) o[c] = dpp_d<0x4E>(s[c]);  // lane ^ 2: the other column's sum
     if (q != 0 || j >= a.P) continue;
     double gv[n];
 #pragma unroll
@@ -995,6 +995,19 @@ __device__ __forceinline__ void backward(const GnArgs& a, const SmemLayout& SL, 
 
 #include "mhe_big.h"
 
+// Inside the Gauss-Newton loop every phase recomputes the layouts (and the
+// table pointers derived from them) from opaque copies of the dimensions
+// instead of keeping ~40 derived 64-bit offsets live in SGPRs across the
+// factorization, whose broadcasts need the scalar registers (SGPR spills to
+// VGPR lanes otherwise push VGPRs to scratch).
+__device__ __forceinline__ int opaque_s(int x) {
+  asm volatile("" : "+s"(x));
+  return x;
+}
+#define FA a
+#define FCL const_layout(opaque_s(a.P), opaque_s(a.M), n, MEAS::p, opaque_s(a.NT))
+#define FSL smem_layout(opaque_s(a.P), opaque_s(a.M), n, opaque_s(a.NT), !MEAS::LINEAR)
+
 template <class DYN, class MEAS, int SLOTS, int mode, bool HUBER = false>
 __global__ __launch_bounds__(NTHREADS, NW / 2) void k_gn(GnArgs a) {  // 2nd arg: min waves per SIMD (2 WGs per CU)
   constexpr int n = DYN::n;
@@ -1036,16 +1049,16 @@ __global__ __launch_bounds__(NTHREADS, NW / 2) void k_gn(GnArgs a) {  // 2nd arg
   DIAG_DECL
   for (;;) {
     DIAG_MARK(7);
-    double c1 = node_phase<DYN, HUBER>(a, CL, SL, sm, b);
-    c1 += meas_phase<DYN, MEAS>(a, CL, SL, sm, b);
+    double c1 = node_phase<DYN, HUBER>(FA, FCL, FSL, sm, opaque_s(b));
+    c1 += meas_phase<DYN, MEAS>(FA, FCL, FSL, sm, opaque_s(b));
     __syncthreads();
     DIAG_MARK(0);
-    c1 += grad_phase<DYN>(a, CL, SL, sm, b);
+    c1 += grad_phase<DYN>(FA, FCL, FSL, sm, opaque_s(b));
     DIAG_MARK(1);
     if constexpr (mode == MODE_ASSEMBLE) {
       double c2 = 0.0;
       block_reduce2(RED, c1, c2, false);
-      build_tiles<DYN, MEAS, SLOTS, HUBER>(a, CL, SL, sm, acc, wave, lane, stab);
+      build_tiles<DYN, MEAS, SLOTS, HUBER>(FA, FCL, FSL, sm, acc, wave, lane, stab);
       const int dp = 16 * a.NT;
       double* Hb = a.Hout + (size_t)b * dp * dp;
 #pragma unroll
@@ -1071,16 +1084,16 @@ __global__ __launch_bounds__(NTHREADS, NW / 2) void k_gn(GnArgs a) {  // 2nd arg
       return;
     }
     if (it >= a.max_iter) break;
-    build_tiles<DYN, MEAS, SLOTS, HUBER>(a, CL, SL, sm, acc, wave, lane, stab);
+    build_tiles<DYN, MEAS, SLOTS, HUBER>(FA, FCL, FSL, sm, acc, wave, lane, stab);
     __syncthreads();
     DIAG_MARK(2);
-    const bool ok = factor_forward<SLOTS>(a, SL, sm, acc, wave, lane, stab, DIAG_FARGS);
+    const bool ok = factor_forward<SLOTS>(FA, FSL, sm, acc, wave, lane, stab, DIAG_FARGS);
     DIAG_MARK(3);
     if (!ok) {
       status = MHE_STATUS_NOT_SPD;
       break;
     }
-    backward<SLOTS>(a, SL, sm, acc, wave, lane, stab);
+    backward<SLOTS>(FA, FSL, sm, acc, wave, lane, stab);
     DIAG_MARK(4);
     // X += delta, projected onto the bounds (addVarBounds); the convergence test uses
     // |delta| for unclipped components and the actual move for clipped ones.  A
@@ -1115,10 +1128,10 @@ __global__ __launch_bounds__(NTHREADS, NW / 2) void k_gn(GnArgs a) {  // 2nd arg
     if (dmax <= a.tol * (1.0 + xmax)) {
       status = MHE_STATUS_CONVERGED;
       // final cost at the converged iterate
-      double cf = node_phase<DYN, HUBER>(a, CL, SL, sm, b);
-      cf += meas_phase<DYN, MEAS>(a, CL, SL, sm, b);
+      double cf = node_phase<DYN, HUBER>(FA, FCL, FSL, sm, opaque_s(b));
+      cf += meas_phase<DYN, MEAS>(FA, FCL, FSL, sm, opaque_s(b));
       __syncthreads();
-      cf += grad_phase<DYN>(a, CL, SL, sm, b);
+      cf += grad_phase<DYN>(FA, FCL, FSL, sm, opaque_s(b));
       double z = 0.0;
       block_reduce2(RED, cf, z, false);
       if (threadIdx.x == 0) a.cost[b] = cf;
@@ -1128,10 +1141,10 @@ __global__ __launch_bounds__(NTHREADS, NW / 2) void k_gn(GnArgs a) {  // 2nd arg
   {
     // cost at the returned iterate (the loop's last residual pass is at Xs
     // unless the iteration broke before updating)
-    double cf = node_phase<DYN, HUBER>(a, CL, SL, sm, b);
-    cf += meas_phase<DYN, MEAS>(a, CL, SL, sm, b);
+    double cf = node_phase<DYN, HUBER>(FA, FCL, FSL, sm, opaque_s(b));
+    cf += meas_phase<DYN, MEAS>(FA, FCL, FSL, sm, opaque_s(b));
     __syncthreads();
-    cf += grad_phase<DYN>(a, CL, SL, sm, b);
+    cf += grad_phase<DYN>(FA, FCL, FSL, sm, opaque_s(b));
     double z = 0.0;
     block_reduce2(RED, cf, z, false);
     if (threadIdx.x == 0) a.cost[b] = cf;
@@ -1146,6 +1159,9 @@ done:
     a.status[b] = status;
   }
 }
+#undef FA
+#undef FCL
+#undef FSL
 
 // ------------------------------------------------------------ constants
 // Cc tile element (row, col) of the constant part of J^T W J.
