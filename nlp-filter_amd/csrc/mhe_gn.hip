@@ -1050,7 +1050,9 @@ __global__ __launch_bounds__(NTHREADS, NW / 2) void k_gn(GnArgs a) {  // 2nd arg
   for (;;) {
     DIAG_MARK(7);
     double c1 = node_phase<DYN, HUBER>(FA, FCL, FSL, sm, opaque_s(b));
+    DIAG_MARK(6);
     c1 += meas_phase<DYN, MEAS>(FA, FCL, FSL, sm, opaque_s(b));
+    DIAG_MARK(14);
     __syncthreads();
     DIAG_MARK(0);
     c1 += grad_phase<DYN>(FA, FCL, FSL, sm, opaque_s(b));
