@@ -305,21 +305,14 @@ __device__ __forceinline__ void dot_rows_part(const double* __restrict__ Mt, int
 //   W_k = a * sum_j D_kj X_j - f(X_k, U_k);  V_k = c_k Qw W_k;  E_k = c_k Qw F_k;
 //   FtE_k = F_k^T E_k;  FtV_k = F_k^T V_k;   cost += c_k W_k^T Qw W_k
 template <class DYN, bool HUBER = false>
-__device__ __forceinline__ double node_phase(const GnArgs& a, const ConstLayout& CL, const SmemLayout& SL, double* sm, int b) {
+__device__ __forceinline__ double node_row(const GnArgs& a, const ConstLayout& CL, const SmemLayout& SL, double* sm,
+                                           int b, int k, const double (&dx)[DYN::n]) {
   constexpr int n = DYN::n, m = DYN::m;
-  const double* Dt = (const double*)(a.cbuf + CL.Dt);
   const double* cw = (const double*)(a.cbuf + CL.cw);
   const double* Qw = (const double*)(a.cbuf + CL.Qw);
   const double* Xs = sm + SL.Xs;
   double cost = 0.0;
-  const int tid = opaque_tid();
-  const int part = tid % TPR;
-  for (int k0 = 0; k0 < a.P; k0 += NTHREADS / TPR) {
-    const int k = k0 + tid / TPR;
-    const int kk = k < a.P ? k : a.P - 1;
-    double dx[n];
-    dot_rows_part<n>(Dt, a.P, kk, a.P, part, Xs, dx);
-    if (part || k >= a.P) continue;
+  {
     double xk[n], uk[m > 0 ? m : 1], f[n], F[n * n];
 #pragma unroll
     for (int c = 0; c < n; ++c) xk[c] = Xs[k * n + c];
@@ -392,24 +385,35 @@ __device__ __forceinline__ double node_phase(const GnArgs& a, const ConstLayout&
   return cost;
 }
 
-// Per-measurement-row quantities (nlp/nlp.py:264-273):
-//   x_i = sum_j Phi_ij X_j;  e_i = y_i - h(x_i);  GE_i = H_i^T Rw_i e_i;
-//   (nonlinear) G_i = H_i^T Rw_i H_i;  cost += e_i^T Rw_i e_i
-template <class DYN, class MEAS>
-__device__ __forceinline__ double meas_phase(const GnArgs& a, const ConstLayout& CL, const SmemLayout& SL, double* sm, int b) {
-  constexpr int n = DYN::n, p = MEAS::p, q = MEAS::q;
-  const double* PhiT = (const double*)(a.cbuf + CL.PhiT);
-  const double* Rw = (const double*)(a.cbuf + CL.Rw);
+template <class DYN, bool HUBER = false>
+__device__ __forceinline__ double node_phase(const GnArgs& a, const ConstLayout& CL, const SmemLayout& SL, double* sm, int b) {
+  constexpr int n = DYN::n;
+  const double* Dt = (const double*)(a.cbuf + CL.Dt);
   const double* Xs = sm + SL.Xs;
   double cost = 0.0;
   const int tid = opaque_tid();
   const int part = tid % TPR;
-  for (int i0 = 0; i0 < a.M; i0 += NTHREADS / TPR) {
-    const int i = i0 + tid / TPR;
-    const int ii = i < a.M ? i : a.M - 1;
-    double xi[n];
-    dot_rows_part<n>(PhiT, a.M, ii, a.P, part, Xs, xi);
-    if (part || i >= a.M) continue;
+  for (int k0 = 0; k0 < a.P; k0 += NTHREADS / TPR) {
+    const int k = k0 + tid / TPR;
+    const int kk = k < a.P ? k : a.P - 1;
+    double dx[n];
+    dot_rows_part<n>(Dt, a.P, kk, a.P, part, Xs, dx);
+    if (part || k >= a.P) continue;
+    cost += node_row<DYN, HUBER>(a, CL, SL, sm, b, k, dx);
+  }
+  return cost;
+}
+
+// Per-measurement-row quantities (nlp/nlp.py:264-273):
+//   x_i = sum_j Phi_ij X_j;  e_i = y_i - h(x_i);  GE_i = H_i^T Rw_i e_i;
+//   (nonlinear) G_i = H_i^T Rw_i H_i;  cost += e_i^T Rw_i e_i
+template <class DYN, class MEAS>
+__device__ __forceinline__ double meas_row(const GnArgs& a, const ConstLayout& CL, const SmemLayout& SL, double* sm,
+                                           int b, int i, const double (&xi)[DYN::n]) {
+  constexpr int n = DYN::n, p = MEAS::p, q = MEAS::q;
+  const double* Rw = (const double*)(a.cbuf + CL.Rw);
+  double cost = 0.0;
+  {
     double par[q > 0 ? q : 1];
     if (q > 0) {
       const double* PR = a.PAR + (long long)b * a.pstride + (long long)i * q;
@@ -467,6 +471,89 @@ __device__ __forceinline__ double meas_phase(const GnArgs& a, const ConstLayout&
           G[r * n + c] = s;
         }
     }
+  }
+  return cost;
+}
+
+template <class DYN, class MEAS>
+__device__ __forceinline__ double meas_phase(const GnArgs& a, const ConstLayout& CL, const SmemLayout& SL, double* sm, int b) {
+  constexpr int n = DYN::n;
+  const double* PhiT = (const double*)(a.cbuf + CL.PhiT);
+  const double* Xs = sm + SL.Xs;
+  double cost = 0.0;
+  const int tid = opaque_tid();
+  const int part = tid % TPR;
+  for (int i0 = 0; i0 < a.M; i0 += NTHREADS / TPR) {
+    const int i = i0 + tid / TPR;
+    const int ii = i < a.M ? i : a.M - 1;
+    double xi[n];
+    dot_rows_part<n>(PhiT, a.M, ii, a.P, part, Xs, xi);
+    if (part || i >= a.M) continue;
+    cost += meas_row<DYN, MEAS>(a, CL, SL, sm, b, i, xi);
+  }
+  return cost;
+}
+
+// node_phase + meas_phase.  When both row counts fit one pass (P, M <= 128 with
+// 4 lanes per row: C1, C2) each lane runs its D-row and Phi-row dots together,
+// 16 L2 loads in flight instead of 8, halving the dependent round trips.
+template <class DYN, class MEAS, bool HUBER = false>
+__device__ __forceinline__ double node_meas_phase(const GnArgs& a, const ConstLayout& CL, const SmemLayout& SL,
+                                                  double* sm, int b) {
+  constexpr int n = DYN::n;
+  constexpr int ROWS = NTHREADS / TPR;
+  if (a.P > ROWS || a.M > ROWS)
+    return node_phase<DYN, HUBER>(a, CL, SL, sm, b) + meas_phase<DYN, MEAS>(a, CL, SL, sm, b);
+  const double* Dt = (const double*)(a.cbuf + CL.Dt);
+  const double* PhiT = (const double*)(a.cbuf + CL.PhiT);
+  const double* Xs = sm + SL.Xs;
+  const int tid = opaque_tid();
+  const int part = tid % TPR, r = tid / TPR;
+  const int kk = r < a.P ? r : a.P - 1, ii = r < a.M ? r : a.M - 1;
+  double dx[n], xi[n];
+#pragma unroll
+  for (int c = 0; c < n; ++c) dx[c] = xi[c] = 0.0;
+  const int len = a.P;
+  int j = part;
+#pragma unroll 1
+  for (; j + TPR * 7 < len; j += TPR * 8) {
+    double m1[8], m2[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      m1[u] = Dt[(j + TPR * u) * a.P + kk];
+      m2[u] = PhiT[(j + TPR * u) * a.M + ii];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+#pragma unroll
+      for (int c = 0; c < n; ++c) {
+        const double x = Xs[(j + TPR * u) * n + c];
+        dx[c] += m1[u] * x;
+        xi[c] += m2[u] * x;
+      }
+  }
+  for (; j < len; j += TPR) {
+    const double m1 = Dt[j * a.P + kk], m2 = PhiT[j * a.M + ii];
+#pragma unroll
+    for (int c = 0; c < n; ++c) {
+      dx[c] += m1 * Xs[j * n + c];
+      xi[c] += m2 * Xs[j * n + c];
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < n; ++c) {
+    dx[c] += dpp_d<0xB1>(dx[c]);
+    xi[c] += dpp_d<0xB1>(xi[c]);
+  }
+#pragma unroll
+  for (int c = 0; c < n; ++c) {
+    dx[c] += dpp_d<0x4E>(dx[c]);
+    xi[c] += dpp_d<0x4E>(xi[c]);
+  }
+  double cost = 0.0;
+  if (part == 0) {
+    if (r < a.P) cost += node_row<DYN, HUBER>(a, CL, SL, sm, b, r, dx);
+    if (r < a.M) cost += meas_row<DYN, MEAS>(a, CL, SL, sm, b, r, xi);
   }
   return cost;
 }
@@ -1049,13 +1136,18 @@ __global__ __launch_bounds__(NTHREADS, NW / 2) void k_gn(GnArgs a) {  // 2nd arg
   DIAG_DECL
   for (;;) {
     DIAG_MARK(7);
-    double c1 = node_phase<DYN, HUBER>(FA, FCL, FSL, sm, opaque_s(b));
+    double c1 = node_meas_phase<DYN, MEAS, HUBER>(FA, FCL, FSL, sm, opaque_s(b));
     DIAG_MARK(6);
-    c1 += meas_phase<DYN, MEAS>(FA, FCL, FSL, sm, opaque_s(b));
     DIAG_MARK(14);
     __syncthreads();
     DIAG_MARK(0);
     c1 += grad_phase<DYN>(FA, FCL, FSL, sm, opaque_s(b));
+    {
+      // park this wave's part of the cost in LDS (a live register across the
+      // factorization would spill): read back if the loop exits at this iterate
+      const double cwv = wave_sum(c1);
+      if (lane == 0) RED[2 * NW + wave] = cwv;
+    }
     DIAG_MARK(1);
     if constexpr (mode == MODE_ASSEMBLE) {
       double c2 = 0.0;
@@ -1130,8 +1222,7 @@ __global__ __launch_bounds__(NTHREADS, NW / 2) void k_gn(GnArgs a) {  // 2nd arg
     if (dmax <= a.tol * (1.0 + xmax)) {
       status = MHE_STATUS_CONVERGED;
       // final cost at the converged iterate
-      double cf = node_phase<DYN, HUBER>(FA, FCL, FSL, sm, opaque_s(b));
-      cf += meas_phase<DYN, MEAS>(FA, FCL, FSL, sm, opaque_s(b));
+      double cf = node_meas_phase<DYN, MEAS, HUBER>(FA, FCL, FSL, sm, opaque_s(b));
       __syncthreads();
       cf += grad_phase<DYN>(FA, FCL, FSL, sm, opaque_s(b));
       double z = 0.0;
@@ -1141,15 +1232,14 @@ __global__ __launch_bounds__(NTHREADS, NW / 2) void k_gn(GnArgs a) {  // 2nd arg
     }
   }
   {
-    // cost at the returned iterate (the loop's last residual pass is at Xs
-    // unless the iteration broke before updating)
-    double cf = node_phase<DYN, HUBER>(FA, FCL, FSL, sm, opaque_s(b));
-    cf += meas_phase<DYN, MEAS>(FA, FCL, FSL, sm, opaque_s(b));
+    // every other exit (max_iter, non-SPD pivot, non-finite step) leaves Xs at the
+    // iterate of the loop's last residual pass: its cost is already summed
     __syncthreads();
-    cf += grad_phase<DYN>(FA, FCL, FSL, sm, opaque_s(b));
-    double z = 0.0;
-    block_reduce2(RED, cf, z, false);
-    if (threadIdx.x == 0) a.cost[b] = cf;
+    if (threadIdx.x == 0) {
+      double cf = RED[2 * NW];
+      for (int w = 1; w < NW; ++w) cf += RED[2 * NW + w];
+      a.cost[b] = cf;
+    }
   }
 done:
   DIAG_MARK(5);
