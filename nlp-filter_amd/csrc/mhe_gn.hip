@@ -696,7 +696,12 @@ __device__ __forceinline__ void build_tiles(const GnArgs& a, const ConstLayout& 
   for (int s = 0; s < SLOTS; ++s) {
     const int IJ = slot_ij(stab, s);
     if (IJ < 0) {
-      acc[s] = d4{0.0, 0.0, 0.0, 0.0};  // no tile: always define (keeps acc dead between iterations)
+      // no tile: always define (keeps acc dead between iterations), but with an
+      // opaque value -- a zero constant would be hoisted out of the Gauss-Newton
+      // loop and kept live (spilled) across the factorization.  Never read.
+      d4 junk;
+      asm volatile("" : "=v"(junk));
+      acc[s] = junk;
     } else {
       const int I = IJ & 0xffff, J = IJ >> 16;
       const size_t off = (size_t)tile_index(I, J, a.NT) * 256 + lane;
