@@ -3,13 +3,13 @@
 // What replaces what (reference kingdwd/nlp-filter):
 //   fixedTimeOptimalEstimationNLP objective   nlp/nlp.py:202-286
 //   NLP.solve() -> CasADi/IPOPT               nlp/nlp.py:61-83
-// is re-built here as ONE fused kernel per batch: one workgroup (4 waves) per
+// is re-built here as ONE fused kernel per batch: one workgroup (8 waves) per
 // trajectory runs the whole Gauss-Newton loop
 //     residual + Jacobian  ->  J^T W J, J^T W r  ->  Cholesky  ->  2 triangular
 //     solves  ->  X += delta  ->  convergence test
 // with the d x d normal matrix (d = (N+1) n, padded to 16*NT) held in the MFMA
-// accumulator registers of the 4 waves as 16x16 fp64 tiles (lower triangle,
-// 2 KB per tile, 8 VGPRs per lane).  The right-looking blocked Cholesky
+// accumulator registers of the 8 waves as 16x16 fp64 tiles (off-diagonal tiles,
+// 2 KB per tile, 8 VGPRs per lane; diagonal tiles in LDS).  The right-looking blocked Cholesky
 // factors one 16-column panel per step in registers (row-per-lane sweep with
 // scalar broadcasts), streams the panel through LDS and applies the trailing
 // update with v_mfma_f64_16x16x4f64.  The forward solve rides along with the
