@@ -92,11 +92,24 @@ def cpu_baseline(w, iters, sample_B, target_s=10.0):
             dt = time.perf_counter() - t0
             if dt >= target_s:
                 break
+    # SURVEY.md 8(d) also asks for the 1-core figure: a 64-trajectory slice, ~3 s
+    one = np.arange(min(64, B))
+    with threadpool_limits(1):
+        work(one[:2])
+        t1, reps1 = time.perf_counter(), 0
+        while True:
+            work(one)
+            reps1 += 1
+            dt1 = time.perf_counter() - t1
+            if dt1 >= target_s / 3:
+                break
     return {"value": reps * B * w.P * iters / dt, "unit": "GN collocation-point updates/s", "cores": cores,
             "kind": "port",
+            "value_1core": reps1 * len(one) * w.P * iters / dt1,
             "sample": f"{reps} x ({B} of the {w.B} C2 trajectories x {iters} GN iterations) with oracle.gn.CpuPort "
                       f"(same algorithm: constant J^T W J part precomputed, LAPACK dpotrf + 2 trsv per trajectory), "
-                      f"{cores} worker threads, {dt:.1f} s wall"}
+                      f"{cores} worker threads, {dt:.1f} s wall; value_1core: {reps1} x {len(one)} trajectories "
+                      f"x {iters} iterations on one thread, {dt1:.1f} s"}
 
 
 def main():
