@@ -264,6 +264,10 @@ typedef struct mhe_ekf_dims {
   int32_t dyn_model;   /* MHE_EKF_DYN_* */
   int32_t meas_model;  /* MHE_EKF_MEAS_* */
   double dt;           /* dyn_func_params["dt"] */
+  int32_t r_diag;      /* 1: the caller guarantees every step's R block is diagonal -> the
+                          correction runs as sequential scalar updates, one filter per lane
+                          (same result as the batch update up to rounding); 0: general R,
+                          one wavefront per filter with an augmented Cholesky sweep */
 } mhe_ekf_dims;
 
 /*

@@ -246,10 +246,118 @@ __global__ __launch_bounds__(NWF * 64) void k_ekf(EkfArgs a) {
   if (a.status && lane == 0) a.status[b] = status;
 }
 
+// ---------------------------------------------------------------- one filter per lane
+// When every step's R is diagonal (dims->r_diag, checked by the caller) the
+// correction is done as nz sequential SCALAR updates, all linearised at the
+// prediction mu- (row i: h_i, H_i at mu-; innovation e_i = z_i - h_i(mu-) -
+// H_i (mu - mu-) against the running mean).  For a linear(ised) measurement
+// model with diagonal R this is algebraically the reference's batch update
+// (utils/ekf.py:51-59: K = S- H^T P^-1, mu = mu- + K e, S = S- - K H S-):
+//   v = S H_i^T,  s = H_i v + R_ii,  mu += v e_i / s,  S -= v v^T / s.
+// The whole filter lives in one lane's registers (mu, mu-, S: 35 doubles), so a
+// wave runs 64 filters with no broadcasts, barriers or LDS: O(p n^2) work per
+// step instead of the sweep's O(p^3), and no lane idles on the row loop.
 template <class DYN, class MEAS>
-int launch(EkfArgs& a, hipStream_t st) {
-  const int smem = NWF * WaveSmem<DYN::n>::total * (int)sizeof(double);
-  hipLaunchKernelGGL((k_ekf<DYN, MEAS>), dim3((a.batch + NWF - 1) / NWF), dim3(NWF * 64), smem, st, a);
+__global__ __launch_bounds__(256) void k_ekf_lane(EkfArgs a) {
+  constexpr int n = DYN::n, m = DYN::m, q = MEAS::q;
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= a.batch) return;  // no barriers below
+  double mu[n], S[n * n];
+#pragma unroll
+  for (int c = 0; c < n; ++c) mu[c] = a.mu[(size_t)b * n + c];
+#pragma unroll
+  for (int c = 0; c < n * n; ++c) S[c] = a.S[(size_t)b * n * n + c];
+  int status = 0;
+  for (int k = 0; k < a.steps; ++k) {
+    // ---- predict: mu- = f(mu, u), S- = G S G^T + Q   (utils/ekf.py:40-45)
+    double u[m > 0 ? m : 1], mp[n], G[n * n];
+    const double* up = a.U + (long long)b * a.u_bstride + (long long)k * m;
+#pragma unroll
+    for (int c = 0; c < m; ++c) u[c] = up[c];
+    DYN::step(mu, u, a.dt, mp, G);
+    double GS[n * n];
+#pragma unroll
+    for (int r = 0; r < n; ++r)
+#pragma unroll
+      for (int c = 0; c < n; ++c) {
+        double acc = 0.0;
+#pragma unroll
+        for (int l = 0; l < n; ++l) acc += G[r * n + l] * S[l * n + c];
+        GS[r * n + c] = acc;
+      }
+#pragma unroll
+    for (int r = 0; r < n; ++r)
+#pragma unroll
+      for (int c = 0; c < n; ++c) {
+        double acc = 0.0;
+#pragma unroll
+        for (int l = 0; l < n; ++l) acc += GS[r * n + l] * G[c * n + l];
+        S[r * n + c] = acc + a.Q[r * n + c];
+      }
+#pragma unroll
+    for (int c = 0; c < n; ++c) mu[c] = mp[c];
+    // ---- correct: sequential scalar updates at the linearisation point mu-
+    const int nz = a.nz[(long long)b * a.nz_bstride + k];
+    if (nz > MAXP) status = 2;
+    const int rows = nz <= MAXP ? nz : 0;
+    const double* zk = a.Z + (long long)b * a.z_bstride + (long long)k * a.nmeas_rows_max;
+    const double* pk = a.PAR + (long long)b * a.par_bstride + (long long)k * a.nmeas_rows_max * q;
+    const double* Rk = a.R + (long long)b * a.r_bstride + (long long)k * a.r_sstride;
+    for (int i = 0; i < rows; ++i) {
+      double h, H[n];
+      MEAS::template row<n>(mp, pk + i * q, i, nz, h, H);
+      double e = zk[i] - h;
+#pragma unroll
+      for (int c = 0; c < n; ++c) e -= H[c] * (mu[c] - mp[c]);
+      double v[n];
+#pragma unroll
+      for (int r = 0; r < n; ++r) {
+        double acc = 0.0;
+#pragma unroll
+        for (int c = 0; c < n; ++c) acc += S[r * n + c] * H[c];
+        v[r] = acc;
+      }
+      double sv = Rk[i * a.nmeas_rows_max + i];
+#pragma unroll
+      for (int c = 0; c < n; ++c) sv += H[c] * v[c];
+      if (!(sv > 0.0 && sv < INFINITY)) status = 1;
+      const double inv = 1.0 / sv;
+      const double ge = e * inv;
+#pragma unroll
+      for (int r = 0; r < n; ++r) mu[r] += v[r] * ge;
+#pragma unroll
+      for (int r = 0; r < n; ++r) {
+        const double vr = v[r] * inv;
+#pragma unroll
+        for (int c = 0; c < n; ++c) S[r * n + c] -= vr * v[c];
+      }
+    }
+    if (a.mu_hist) {
+      double* mh = a.mu_hist + ((size_t)b * a.steps + k) * n;
+#pragma unroll
+      for (int c = 0; c < n; ++c) mh[c] = mu[c];
+    }
+    if (a.S_hist) {
+      double* sh = a.S_hist + ((size_t)b * a.steps + k) * n * n;
+#pragma unroll
+      for (int c = 0; c < n * n; ++c) sh[c] = S[c];
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < n; ++c) a.mu[(size_t)b * n + c] = mu[c];
+#pragma unroll
+  for (int c = 0; c < n * n; ++c) a.S[(size_t)b * n * n + c] = S[c];
+  if (a.status) a.status[b] = status;
+}
+
+template <class DYN, class MEAS>
+int launch(EkfArgs& a, hipStream_t st, bool r_diag) {
+  if (r_diag) {
+    hipLaunchKernelGGL((k_ekf_lane<DYN, MEAS>), dim3((a.batch + 255) / 256), dim3(256), 0, st, a);
+  } else {
+    const int smem = NWF * WaveSmem<DYN::n>::total * (int)sizeof(double);
+    hipLaunchKernelGGL((k_ekf<DYN, MEAS>), dim3((a.batch + NWF - 1) / NWF), dim3(NWF * 64), smem, st, a);
+  }
   return hipGetLastError() == hipSuccess ? MHE_OK : MHE_ERR_HIP;
 }
 
@@ -276,9 +384,9 @@ extern "C" int mhe_ekf_run(const mhe_ekf_dims* dims, int32_t batch, int32_t step
   if (!PAR) return MHE_ERR_NULL;
   switch (dims->meas_model) {
     case MHE_EKF_MEAS_MULTI_PSEUDORANGE:
-      return launch<EkfGnssPosAndBias, EkfMultiPseudorange<false>>(a, st);
+      return launch<EkfGnssPosAndBias, EkfMultiPseudorange<false>>(a, st, dims->r_diag != 0);
     case MHE_EKF_MEAS_MULTI_PSEUDORANGE_AND_BIAS:
-      return launch<EkfGnssPosAndBias, EkfMultiPseudorange<true>>(a, st);
+      return launch<EkfGnssPosAndBias, EkfMultiPseudorange<true>>(a, st, dims->r_diag != 0);
   }
   return MHE_ERR_MODEL;
 }

@@ -43,14 +43,18 @@ def _ptr(t):
 
 
 def run_batch(dyn_func, meas_func, mu0, S0, U, Z, nz, Q, R, dt, sat_pos, device=None, stream=None,
-              keep_history=True):
+              keep_history=True, method="auto"):
     """Run B independent filters for T steps in one launch.
 
     mu0 (B,n), S0 (B,n,n), U (B,T,m), Z (B,T,pmax), nz (B,T) valid rows per step
     (0 = predict only), Q (n,n), R (T,pmax,pmax) or (B,T,pmax,pmax), sat_pos
     (B,T,pmax,3); dt = dyn_func_params["dt"].  Inputs may be NumPy or torch.
     Returns (mu_hist (B,T,n), S_hist (B,T,n,n), mu (B,n), S (B,n,n), status (B))
-    as torch tensors on the device."""
+    as torch tensors on the device.
+
+    method: "lane" (diagonal R: sequential scalar updates, one filter per lane),
+    "wave" (any R: one wavefront per filter, augmented Cholesky sweep) or "auto"
+    (lane when every R block is diagonal -- one device-side check)."""
     import torch
 
     (did, n, m), (mid, _, q) = models(dyn_func, meas_func)
@@ -85,7 +89,15 @@ def run_batch(dyn_func, meas_func, mu0, S0, U, Z, nz, Q, R, dt, sat_pos, device=
     mh = torch.empty((B, T, n), dtype=torch.float64, device=dev) if keep_history else None
     Sh = torch.empty((B, T, n, n), dtype=torch.float64, device=dev) if keep_history else None
     st = torch.empty(B, dtype=torch.int32, device=dev)
-    dims = _lib.MheEkfDims(n=n, m=m, pmax=pmax, q=q, dyn_model=did, meas_model=mid, dt=float(dt))
+    if method == "auto":
+        offd = Rt - torch.diag_embed(torch.diagonal(Rt, dim1=-2, dim2=-1))
+        r_diag = Rt.numel() == 0 or not bool((offd != 0).any().item())
+    elif method in ("lane", "wave"):
+        r_diag = method == "lane"
+    else:
+        raise ValueError(f"unknown method {method!r}")
+    dims = _lib.MheEkfDims(n=n, m=m, pmax=pmax, q=q, dyn_model=did, meas_model=mid, dt=float(dt),
+                           r_diag=int(r_diag))
     lib = _lib.load()
     sh = stream.cuda_stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
     rc = lib.mhe_ekf_run(ctypes.byref(dims), B, T, _ptr(mu), _ptr(S), _ptr(Ut), T * m, _ptr(Zt), T * pmax,

@@ -124,12 +124,15 @@ def test_ekf_class_matches_reference_fixture(golden):
 
 
 @pytest.mark.gpu
-def test_ekf_batch_matches_oracle_per_instance(golden):
+@pytest.mark.parametrize("method", ["lane", "wave", "auto"])
+def test_ekf_batch_matches_oracle_per_instance(golden, method):
+    """Both device formulations: sequential scalar updates one filter per lane
+    (diagonal R) and the per-wavefront augmented Cholesky sweep (any R)."""
     fx = _fixture(golden)
     B = 64
     mu0, S0, U, Z, nz, sat, R = _batch_inputs(fx, B, drop_steps=(5, 6, 30))
     mh, Sh, mu, S, st = ekf.run_batch(gnss.gnss_pos_and_bias, gnss.multi_pseudorange, mu0, S0, U, Z, nz,
-                                      fx["Q"], R, 1.0, sat)
+                                      fx["Q"], R, 1.0, sat, method=method)
     assert int(st.abs().sum().item()) == 0
     rmu, rS = _oracle_batch(fx, mu0, S0, U, Z, nz, sat)
     emu, eS = _close(mh.cpu().numpy(), Sh.cpu().numpy(), rmu, rS)
@@ -141,7 +144,8 @@ def test_ekf_batch_matches_oracle_per_instance(golden):
 
 
 @pytest.mark.gpu
-def test_ekf_bias_row_variant(golden):
+@pytest.mark.parametrize("method", ["lane", "wave"])
+def test_ekf_bias_row_variant(golden, method):
     fx = _fixture(golden)
     B = 8
     mu0, S0, U, Z0, nz0, sat, _ = _batch_inputs(fx, B, seed=5)
@@ -157,7 +161,7 @@ def test_ekf_bias_row_variant(golden):
     sat13 = np.zeros((B, T, 13, 3))
     sat13[:, :, :12] = sat
     mh, Sh, _, _, st = ekf.run_batch(gnss.gnss_pos_and_bias, gnss.multi_pseudorange_and_bias, mu0, S0, U, Z, nz,
-                                     fx["Q"], R, 1.0, sat13)
+                                     fx["Q"], R, 1.0, sat13, method=method)
     assert int(st.abs().sum().item()) == 0
     rmu, rS = _oracle_batch(fx, mu0, S0, U, Z, nz, sat13, meas=oekf.multi_pseudorange_and_bias, extra=1)
     emu, eS = _close(mh.cpu().numpy(), Sh.cpu().numpy(), rmu, rS)
@@ -193,3 +197,29 @@ def test_ekf_end_to_end_from_log_files():
                      {"sat_pos": sat})
             emu, eS = _close(mh[b, k].cpu().numpy()[None], Sh[b, k].cpu().numpy()[None], f.mu[None], f.S[None])
             assert emu <= MU_TOL and eS <= S_TOL, (b, k, emu, eS)
+
+
+@pytest.mark.gpu
+def test_ekf_correlated_R_uses_general_path(golden):
+    """A non-diagonal R (correlated pseudorange errors) must take the general
+    per-wavefront sweep under method="auto" and match the oracle's batch update."""
+    fx = _fixture(golden)
+    B = 8
+    mu0, S0, U, Z, nz, sat, _ = _batch_inputs(fx, B, seed=9)
+    T = Z.shape[1]
+    r = float(fx["r_pr"])
+    Rc = r * (0.7 * np.eye(12) + 0.3 * np.ones((12, 12)))
+    R = np.stack([Rc for _ in range(T)])
+    mh, Sh, _, _, st = ekf.run_batch(gnss.gnss_pos_and_bias, gnss.multi_pseudorange, mu0, S0, U, Z, nz,
+                                     fx["Q"], R, 1.0, sat)
+    assert int(st.abs().sum().item()) == 0
+    mus = np.zeros((B, T, 5))
+    Ss = np.zeros((B, T, 5, 5))
+    for b in range(B):
+        f = oekf.EKF(oekf.gnss_pos_and_bias, oekf.multi_pseudorange, mu0[b], S0[b])
+        for k in range(T):
+            ns = int(nz[b, k])
+            f.update(U[b, k], Z[b, k, :ns], fx["Q"], Rc[:ns, :ns], {"dt": 1.0}, None, {"sat_pos": sat[b, k, :ns]})
+            mus[b, k], Ss[b, k] = f.mu, f.S
+    emu, eS = _close(mh.cpu().numpy(), Sh.cpu().numpy(), mus, Ss)
+    assert emu <= MU_TOL and eS <= S_TOL, (emu, eS)
