@@ -268,6 +268,9 @@ typedef struct mhe_ekf_dims {
                           correction runs as sequential scalar updates, one filter per lane
                           (same result as the batch update up to rounding); 0: general R,
                           one wavefront per filter with an augmented Cholesky sweep */
+  int32_t hist_batch_inner; /* 1: mu_hist is (steps, n, B) and S_hist (steps, n, n, B) --
+                               batch innermost, so a wavefront's history stores coalesce;
+                               0: (B, steps, n) / (B, steps, n, n) as below */
 } mhe_ekf_dims;
 
 /*

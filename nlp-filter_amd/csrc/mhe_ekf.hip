@@ -85,8 +85,14 @@ struct EkfArgs {
   long long r_bstride, r_sstride;
   double* mu_hist;
   double* S_hist;
+  int hist_bi;  // 1: histories batch-innermost, mu_hist (steps, n, B), S_hist (steps, n, n, B)
   int* status;
 };
+
+// element (b, k, e) of a per-step history with `w` entries per step
+__device__ __forceinline__ size_t hist_at(const EkfArgs& a, int b, int k, int e, int w) {
+  return a.hist_bi ? ((size_t)k * w + e) * a.batch + b : ((size_t)b * a.steps + k) * w + e;
+}
 
 __device__ __forceinline__ double readlane_d(double v, int lane) {
   const long long b = __double_as_longlong(v);
@@ -237,9 +243,9 @@ __global__ __launch_bounds__(NWF * 64) void k_ekf(EkfArgs a) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     if (a.mu_hist)
-      for (int t = lane; t < n; t += 64) a.mu_hist[((size_t)b * a.steps + k) * n + t] = mu[t];
+      for (int t = lane; t < n; t += 64) a.mu_hist[hist_at(a, b, k, t, n)] = mu[t];
     if (a.S_hist)
-      for (int t = lane; t < n * n; t += 64) a.S_hist[((size_t)b * a.steps + k) * n * n + t] = S[t];
+      for (int t = lane; t < n * n; t += 64) a.S_hist[hist_at(a, b, k, t, n * n)] = S[t];
   }
   for (int t = lane; t < n; t += 64) a.mu[(size_t)b * n + t] = mu[t];
   for (int t = lane; t < n * n; t += 64) a.S[(size_t)b * n * n + t] = S[t];
@@ -303,44 +309,61 @@ __global__ __launch_bounds__(256) void k_ekf_lane(EkfArgs a) {
     const double* zk = a.Z + (long long)b * a.z_bstride + (long long)k * a.nmeas_rows_max;
     const double* pk = a.PAR + (long long)b * a.par_bstride + (long long)k * a.nmeas_rows_max * q;
     const double* Rk = a.R + (long long)b * a.r_bstride + (long long)k * a.r_sstride;
-    for (int i = 0; i < rows; ++i) {
-      double h, H[n];
-      MEAS::template row<n>(mp, pk + i * q, i, nz, h, H);
-      double e = zk[i] - h;
+    // rows in chunks of RCH: all of a chunk's inputs (z, satellite position, R_ii) are
+    // loaded before its first update, so a step costs ceil(nz / RCH) memory round
+    // trips instead of nz (clamped rows read valid memory and are skipped)
+    constexpr int RCH = 8;
+    for (int i0 = 0; i0 < rows; i0 += RCH) {
+      double zr[RCH], pr[RCH][q > 0 ? q : 1], rr[RCH];
 #pragma unroll
-      for (int c = 0; c < n; ++c) e -= H[c] * (mu[c] - mp[c]);
-      double v[n];
+      for (int u = 0; u < RCH; ++u) {
+        const int ic = min(i0 + u, rows - 1);
+        zr[u] = zk[ic];
 #pragma unroll
-      for (int r = 0; r < n; ++r) {
-        double acc = 0.0;
-#pragma unroll
-        for (int c = 0; c < n; ++c) acc += S[r * n + c] * H[c];
-        v[r] = acc;
+        for (int c = 0; c < q; ++c) pr[u][c] = pk[ic * q + c];
+        rr[u] = Rk[ic * a.nmeas_rows_max + ic];
       }
-      double sv = Rk[i * a.nmeas_rows_max + i];
 #pragma unroll
-      for (int c = 0; c < n; ++c) sv += H[c] * v[c];
-      if (!(sv > 0.0 && sv < INFINITY)) status = 1;
-      const double inv = 1.0 / sv;
-      const double ge = e * inv;
+      for (int u = 0; u < RCH; ++u) {
+        if (i0 + u >= rows) break;
+        double h, H[n];
+        MEAS::template row<n>(mp, pr[u], i0 + u, nz, h, H);
+        double e = zr[u] - h;
 #pragma unroll
-      for (int r = 0; r < n; ++r) mu[r] += v[r] * ge;
+        for (int c = 0; c < n; ++c) e -= H[c] * (mu[c] - mp[c]);
+        double v[n];
 #pragma unroll
-      for (int r = 0; r < n; ++r) {
-        const double vr = v[r] * inv;
+        for (int r = 0; r < n; ++r) {
+          double acc = 0.0;
 #pragma unroll
-        for (int c = 0; c < n; ++c) S[r * n + c] -= vr * v[c];
+          for (int c = 0; c < n; ++c) acc += S[r * n + c] * H[c];
+          v[r] = acc;
+        }
+        double sv = rr[u];
+#pragma unroll
+        for (int c = 0; c < n; ++c) sv += H[c] * v[c];
+        if (!(sv > 0.0 && sv < INFINITY)) status = 1;
+        const double inv = 1.0 / sv;
+        const double ge = e * inv;
+#pragma unroll
+        for (int r = 0; r < n; ++r) mu[r] += v[r] * ge;
+#pragma unroll
+        for (int r = 0; r < n; ++r) {
+          const double vr = v[r] * inv;
+#pragma unroll
+          for (int c = 0; c < n; ++c) S[r * n + c] -= vr * v[c];
+        }
       }
     }
+    // histories: with the batch-innermost layout (hist_bi) consecutive lanes write
+    // consecutive words -- one coalesced 512-B store per entry instead of 64 partial lines
     if (a.mu_hist) {
-      double* mh = a.mu_hist + ((size_t)b * a.steps + k) * n;
 #pragma unroll
-      for (int c = 0; c < n; ++c) mh[c] = mu[c];
+      for (int c = 0; c < n; ++c) a.mu_hist[hist_at(a, b, k, c, n)] = mu[c];
     }
     if (a.S_hist) {
-      double* sh = a.S_hist + ((size_t)b * a.steps + k) * n * n;
 #pragma unroll
-      for (int c = 0; c < n * n; ++c) sh[c] = S[c];
+      for (int c = 0; c < n * n; ++c) a.S_hist[hist_at(a, b, k, c, n * n)] = S[c];
     }
   }
 #pragma unroll
@@ -378,6 +401,7 @@ extern "C" int mhe_ekf_run(const mhe_ekf_dims* dims, int32_t batch, int32_t step
   a.mu = mu; a.S = S; a.U = U; a.u_bstride = u_bstride; a.Z = Z; a.z_bstride = z_bstride; a.nz = nz;
   a.nz_bstride = nz_bstride; a.PAR = PAR; a.par_bstride = par_bstride; a.Q = Q; a.R = R; a.r_bstride = r_bstride;
   a.r_sstride = r_sstride; a.mu_hist = mu_hist; a.S_hist = S_hist; a.status = status;
+  a.hist_bi = dims->hist_batch_inner != 0;
   hipStream_t st = (hipStream_t)stream;
   if (dims->dyn_model != MHE_EKF_DYN_GNSS_POS_AND_BIAS || dims->n != 5 || dims->m != 3) return MHE_ERR_MODEL;
   if (dims->q != 3) return MHE_ERR_DIMS;

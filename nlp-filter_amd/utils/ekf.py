@@ -86,8 +86,10 @@ def run_batch(dyn_func, meas_func, mu0, S0, U, Z, nz, Q, R, dt, sat_pos, device=
         r_b, r_s = T * pmax * pmax, pmax * pmax
         if Rt.shape != (B, T, pmax, pmax):
             raise ValueError("R must be (T,pmax,pmax) or (B,T,pmax,pmax)")
-    mh = torch.empty((B, T, n), dtype=torch.float64, device=dev) if keep_history else None
-    Sh = torch.empty((B, T, n, n), dtype=torch.float64, device=dev) if keep_history else None
+    # histories are written batch-innermost (coalesced device stores) and returned as
+    # (B, T, ...) views of that storage
+    mh_st = torch.empty((T, n, B), dtype=torch.float64, device=dev) if keep_history else None
+    Sh_st = torch.empty((T, n, n, B), dtype=torch.float64, device=dev) if keep_history else None
     st = torch.empty(B, dtype=torch.int32, device=dev)
     if method == "auto":
         offd = Rt - torch.diag_embed(torch.diagonal(Rt, dim1=-2, dim2=-1))
@@ -97,13 +99,15 @@ def run_batch(dyn_func, meas_func, mu0, S0, U, Z, nz, Q, R, dt, sat_pos, device=
     else:
         raise ValueError(f"unknown method {method!r}")
     dims = _lib.MheEkfDims(n=n, m=m, pmax=pmax, q=q, dyn_model=did, meas_model=mid, dt=float(dt),
-                           r_diag=int(r_diag))
+                           r_diag=int(r_diag), hist_batch_inner=1)
     lib = _lib.load()
     sh = stream.cuda_stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
     rc = lib.mhe_ekf_run(ctypes.byref(dims), B, T, _ptr(mu), _ptr(S), _ptr(Ut), T * m, _ptr(Zt), T * pmax,
-                         _ptr(nzt), T, _ptr(Pt), T * pmax * q, _ptr(Qt), _ptr(Rt), r_b, r_s, _ptr(mh), _ptr(Sh),
-                         _ptr(st), ctypes.c_void_p(sh))
+                         _ptr(nzt), T, _ptr(Pt), T * pmax * q, _ptr(Qt), _ptr(Rt), r_b, r_s, _ptr(mh_st),
+                         _ptr(Sh_st), _ptr(st), ctypes.c_void_p(sh))
     _lib.check(rc, "mhe_ekf_run")
+    mh = mh_st.permute(2, 0, 1) if keep_history else None
+    Sh = Sh_st.permute(3, 0, 1, 2) if keep_history else None
     return mh, Sh, mu, S, st
 
 
