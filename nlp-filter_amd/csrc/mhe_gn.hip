@@ -42,7 +42,7 @@ enum Mode { MODE_SOLVE = 0, MODE_ASSEMBLE = 1, MODE_LINSOLVE = 2 };
 
 // ------------------------------------------------------------ layouts
 struct ConstLayout {
-  size_t D, Dt, Phi, PhiT, cw, Qw, Pw, Rw, Cc, DA, DB, total;  // byte offsets
+  size_t D, Dt, Phi, PhiT, cw, Qw, Pw, Rw, Cc, DA, DB, DAc, DBc, total;  // byte offsets
 };
 
 __host__ __device__ inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
@@ -62,6 +62,11 @@ __host__ __device__ inline ConstLayout const_layout(int P, int M, int n, int p, 
   L.Cc = o;   o = align256(o + sizeof(double) * ntiles * 256);  // constant part of J^T W J
   L.DA = o;   o = align256(o + sizeof(double) * ntiles * 256);  // a * D[l][j] per tile element
   L.DB = o;   o = align256(o + sizeof(double) * ntiles * 256);  // a * D[j][l] per tile element
+  // n = 2 only: the 8 x 8 node block of D behind each tile, [cn][rn] = a D[8I+cn][8J+rn]
+  // (DAc) and a D[8J+rn][8I+cn] (DBc) -- 512 B per tile instead of 2 KB, spread over
+  // the tile's C layout with ds_bpermute in build_tiles
+  L.DAc = o;  o = align256(o + sizeof(double) * ntiles * 64);
+  L.DBc = o;  o = align256(o + sizeof(double) * ntiles * 64);
   L.total = o;
   return L;
 }
@@ -154,6 +159,14 @@ __device__ __forceinline__ double readlane_d(double v, int lane) {
   const long long b = __double_as_longlong(v);
   const int lo = __builtin_amdgcn_readlane((int)b, lane);
   const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// v of lane (byte_addr / 4), per lane (ds_bpermute: LDS crossbar, no LDS storage)
+__device__ __forceinline__ double bpermute_d(int byte_addr, double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_ds_bpermute(byte_addr, (int)b);
+  const int hi = __builtin_amdgcn_ds_bpermute(byte_addr, (int)(b >> 32));
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
@@ -704,13 +717,29 @@ __device__ __forceinline__ void build_tiles(const GnArgs& a, const ConstLayout& 
       acc[s] = junk;
     } else {
       const int I = IJ & 0xffff, J = IJ >> 16;
-      const size_t off = (size_t)tile_index(I, J, a.NT) * 256 + lane;
+      const int ti = tile_index(I, J, a.NT);
+      const size_t off = (size_t)ti * 256 + lane;
       const int col = 16 * I + (lane & 15);
+      if constexpr (DYN::n == 2) {
+        // a D_lj / a D_jl of element (row, col) = node pair (8I + cn, 8J + rn) of the
+        // tile's 8 x 8 D block, cn = (lane & 15) >> 1, rn = (lane >> 5) + 2r:
+        // one 512-B load per table, then a lane permute per register
+        const double dac = ((const double*)(a.cbuf + CL.DAc))[(size_t)ti * 64 + lane];
+        const double dbc = ((const double*)(a.cbuf + CL.DBc))[(size_t)ti * 64 + lane];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = 16 * J + (lane >> 4) + 4 * r;
-        acc[s][r] = -h_element<DYN, MEAS, HUBER>(a, Phi, Es, FtE, G, Cc[off + 64 * r], DA[off + 64 * r],
-                                                 DB[off + 64 * r], row, col, Dm, LAM);
+        for (int r = 0; r < 4; ++r) {
+          const int row = 16 * J + (lane >> 4) + 4 * r;
+          const int src = (((lane & 15) >> 1) * 8 + (lane >> 5) + 2 * r) * 4;
+          acc[s][r] = -h_element<DYN, MEAS, HUBER>(a, Phi, Es, FtE, G, Cc[off + 64 * r], bpermute_d(src, dac),
+                                                   bpermute_d(src, dbc), row, col, Dm, LAM);
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = 16 * J + (lane >> 4) + 4 * r;
+          acc[s][r] = -h_element<DYN, MEAS, HUBER>(a, Phi, Es, FtE, G, Cc[off + 64 * r], DA[off + 64 * r],
+                                                   DB[off + 64 * r], row, col, Dm, LAM);
+        }
       }
     }
     // bound the scheduler's load hoisting to two slots (register pressure)
@@ -1306,6 +1335,12 @@ __global__ void k_build_cc(int P, int M, int n, int p, int NT, int has_prior, in
   }
   ((double*)(cbuf + CL.DA))[(size_t)t * 256 + r * 64 + lane] = da;
   ((double*)(cbuf + CL.DB))[(size_t)t * 256 + r * 64 + lane] = db;
+  if (r == 0) {
+    const int cn = lane >> 3, rn = lane & 7, l = 8 * I + cn, j = 8 * J + rn;
+    const bool ok = n == 2 && l < P && j < P;
+    ((double*)(cbuf + CL.DAc))[(size_t)t * 64 + lane] = ok ? alpha * D[l * P + j] : 0.0;
+    ((double*)(cbuf + CL.DBc))[(size_t)t * 64 + lane] = ok ? alpha * D[j * P + l] : 0.0;
+  }
 }
 
 __global__ void k_copy_consts(int P, int M, int n, int p, int NT, const double* D, const double* cw,
