@@ -747,14 +747,28 @@ __device__ __forceinline__ void build_tiles(const GnArgs& a, const ConstLayout& 
   }
   double* DT = sm + SL.DT;
   for (int J = wave; J < a.NT; J += NW) {
-    const size_t off = (size_t)tile_index(J, J, a.NT) * 256 + lane;
+    const int ti = tile_index(J, J, a.NT);
+    const size_t off = (size_t)ti * 256 + lane;
     const int col = 16 * J + (lane & 15);
+    double dac = 0.0, dbc = 0.0;
+    if constexpr (DYN::n == 2) {
+      dac = ((const double*)(a.cbuf + CL.DAc))[(size_t)ti * 64 + lane];
+      dbc = ((const double*)(a.cbuf + CL.DBc))[(size_t)ti * 64 + lane];
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int tr = (lane >> 4) + 4 * r;
-      DT[J * DTS + tr * 16 + (lane & 15)] = -h_element<DYN, MEAS, HUBER>(a, Phi, Es, FtE, G, Cc[off + 64 * r],
-                                                                         DA[off + 64 * r], DB[off + 64 * r],
-                                                                         16 * J + tr, col, Dm, LAM);
+      double da, db;
+      if constexpr (DYN::n == 2) {
+        const int src = (((lane & 15) >> 1) * 8 + (lane >> 5) + 2 * r) * 4;
+        da = bpermute_d(src, dac);
+        db = bpermute_d(src, dbc);
+      } else {
+        da = DA[off + 64 * r];
+        db = DB[off + 64 * r];
+      }
+      DT[J * DTS + tr * 16 + (lane & 15)] = -h_element<DYN, MEAS, HUBER>(a, Phi, Es, FtE, G, Cc[off + 64 * r], da,
+                                                                         db, 16 * J + tr, col, Dm, LAM);
     }
   }
 }
