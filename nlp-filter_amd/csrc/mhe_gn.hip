@@ -170,6 +170,18 @@ __device__ __forceinline__ double bpermute_d(int byte_addr, double v) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
+// Raw buffer loads from the constants buffer: one resource (SGPRs) over all of
+// cbuf, a per-lane byte offset and a wave-uniform SGPR offset per unrolled term,
+// so each table element costs one buffer_load and no 64-bit address VALU.
+typedef unsigned int mhe_u2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t cbuf_rsrc(const char* cbuf, size_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)cbuf, (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ double bload(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  const mhe_u2 v = __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0);
+  return __builtin_bit_cast(double, v);
+}
+
 // Butterfly step over lanes within a DPP row: quad_perm xor 1 / xor 2,
 // row_half_mirror, row_mirror -- each leaves every lane of the row holding the
 // combined value of its partner set.  Then v_permlane16/32_swap across rows.
@@ -517,8 +529,7 @@ __device__ __forceinline__ double node_meas_phase(const GnArgs& a, const ConstLa
   constexpr int ROWS = NTHREADS / TPR;
   if (a.P > ROWS || a.M > ROWS)
     return node_phase<DYN, HUBER>(a, CL, SL, sm, b) + meas_phase<DYN, MEAS>(a, CL, SL, sm, b);
-  const double* Dt = (const double*)(a.cbuf + CL.Dt);
-  const double* PhiT = (const double*)(a.cbuf + CL.PhiT);
+  const __amdgpu_buffer_rsrc_t rs = cbuf_rsrc(a.cbuf, CL.total);
   const double* Xs = sm + SL.Xs;
   const int tid = opaque_tid();
   const int part = tid % TPR, r = tid / TPR;
@@ -527,15 +538,20 @@ __device__ __forceinline__ double node_meas_phase(const GnArgs& a, const ConstLa
 #pragma unroll
   for (int c = 0; c < n; ++c) dx[c] = xi[c] = 0.0;
   const int len = a.P;
+  // byte offsets of Dt[j][kk] and PhiT[j][ii]; per term u the uniform offsets u TPR ld 8
+  int o1 = (int)CL.Dt + (part * a.P + kk) * 8, o2 = (int)CL.PhiT + (part * a.M + ii) * 8;
+  const int s1 = TPR * a.P * 8, s2 = TPR * a.M * 8;
   int j = part;
 #pragma unroll 1
   for (; j + TPR * 7 < len; j += TPR * 8) {
     double m1[8], m2[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      m1[u] = Dt[(j + TPR * u) * a.P + kk];
-      m2[u] = PhiT[(j + TPR * u) * a.M + ii];
+      m1[u] = bload(rs, o1, u * s1);
+      m2[u] = bload(rs, o2, u * s2);
     }
+    o1 += 8 * s1;
+    o2 += 8 * s2;
 #pragma unroll
     for (int u = 0; u < 8; ++u)
 #pragma unroll
@@ -546,7 +562,9 @@ __device__ __forceinline__ double node_meas_phase(const GnArgs& a, const ConstLa
       }
   }
   for (; j < len; j += TPR) {
-    const double m1 = Dt[j * a.P + kk], m2 = PhiT[j * a.M + ii];
+    const double m1 = bload(rs, o1, 0), m2 = bload(rs, o2, 0);
+    o1 += s1;
+    o2 += s2;
 #pragma unroll
     for (int c = 0; c < n; ++c) {
       dx[c] += m1 * Xs[j * n + c];
@@ -577,8 +595,7 @@ __device__ __forceinline__ double node_meas_phase(const GnArgs& a, const ConstLa
 template <class DYN>
 __device__ __forceinline__ double grad_phase(const GnArgs& a, const ConstLayout& CL, const SmemLayout& SL, double* sm, int b) {
   constexpr int n = DYN::n;
-  const double* D = (const double*)(a.cbuf + CL.D);
-  const double* Phi = (const double*)(a.cbuf + CL.Phi);
+  const __amdgpu_buffer_rsrc_t rs = cbuf_rsrc(a.cbuf, CL.total);
   const double* Pw = (const double*)(a.cbuf + CL.Pw);
   const double* Vs = sm + SL.Vs;
   const double* FtV = sm + SL.FtV;
@@ -596,25 +613,29 @@ __device__ __forceinline__ double grad_phase(const GnArgs& a, const ConstLayout&
   for (int j0 = 0; j0 < a.P; j0 += NTHREADS / TPR) {
     const int j = j0 + tid / TPR;
     const int jj = j < a.P ? j : a.P - 1;
-    const double* Mt = phi ? Phi : D;
     const double* vec = phi ? GE : Vs;
     const int len = phi ? a.M : a.P;
     double s[n];
 #pragma unroll
     for (int c = 0; c < n; ++c) s[c] = 0.0;
+    // D and Phi share the row stride P: byte offset of Mt[k][jj], uniform step per term
+    int om = (int)(phi ? CL.Phi : CL.D) + (sub * a.P + jj) * 8;
+    const int sm8 = HP * a.P * 8;
     int k = sub;
 #pragma unroll 1
     for (; k + HP * 7 < len; k += HP * 8) {
       double mv[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) mv[u] = Mt[(k + HP * u) * a.P + jj];
+      for (int u = 0; u < 8; ++u) mv[u] = bload(rs, om, u * sm8);
+      om += 8 * sm8;
 #pragma unroll
       for (int u = 0; u < 8; ++u)
 #pragma unroll
         for (int c = 0; c < n; ++c) s[c] += mv[u] * vec[(k + HP * u) * n + c];
     }
     for (; k < len; k += HP) {
-      const double mv = Mt[k * a.P + jj];
+      const double mv = bload(rs, om, 0);
+      om += sm8;
 #pragma unroll
       for (int c = 0; c < n; ++c) s[c] += mv * vec[k * n + c];
     }
