@@ -1131,17 +1131,27 @@ __device__ __forceinline__ void backward(const GnArgs& a, const SmemLayout& SL, 
         const bool crit = J == bb - 1;
         if (crit) __builtin_amdgcn_s_setprio(3);
         double* yj = DV + 16 * J;
+        const int g = lane_o >> 4, c = lane_o & 15;
         double part[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) part[r] = row16_sum(acc[s][r] * db);
-        // lane l of row group g = l>>4 holds the sums for rows g + 4r; lane (l & 15) == r writes row g + 4r
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if ((lane_o & 15) == r) yj[(lane_o >> 4) + 4 * r] -= part[r];
+        // lane l of row group g = l>>4 holds the sums for rows g + 4r
         if (crit) {
-          wave_lds_sync();
-          block_back(DT + J * DTS, yj, lane_o);
+          // delta_J = L_JJ^-T (y_J - U_{J,bb} delta_bb) straight from these registers:
+          // lane (c, g) takes the rows g + 4r it already holds, rows4_sum completes the
+          // dot -- no store / reload of y_J in between
+          const double* LT = DT + J * DTS;
+          double sd = 0.0;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) sd += LT[c * LIS + g + 4 * r] * (yj[g + 4 * r] - part[r]);
+          const double dv = rows4_sum(sd);
+          if (lane_o < 16) yj[c] = dv;  // every lane has read y_J (rows4_sum depends on all of them)
           __builtin_amdgcn_s_setprio(0);
+        } else {
+          // lane (l & 15) == r writes row g + 4r
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (c == r) yj[g + 4 * r] -= part[r];
         }
       }
     }
