@@ -271,6 +271,9 @@ typedef struct mhe_ekf_dims {
   int32_t hist_batch_inner; /* 1: mu_hist is (steps, n, B) and S_hist (steps, n, n, B) --
                                batch innermost, so a wavefront's history stores coalesce;
                                0: (B, steps, n) / (B, steps, n, n) as below */
+  int32_t in_batch_inner;   /* 1: U (steps, m, B), Z (steps, pmax, B), nz (steps, B), PAR
+                               (steps, pmax, q, B) -- batch innermost (coalesced reads; the
+                               *_bstride arguments are ignored); 0: the layouts below */
 } mhe_ekf_dims;
 
 /*

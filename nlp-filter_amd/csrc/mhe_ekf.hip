@@ -86,6 +86,8 @@ struct EkfArgs {
   double* mu_hist;
   double* S_hist;
   int hist_bi;  // 1: histories batch-innermost, mu_hist (steps, n, B), S_hist (steps, n, n, B)
+  long long es;  // element stride of U / Z / nz / PAR: 1 (batch outermost) or batch (batch innermost,
+                 // the b-strides are then 1): entry e of step k of instance b at b*bstride + (k*W + e)*es
   int* status;
 };
 
@@ -137,8 +139,7 @@ __global__ __launch_bounds__(NWF * 64) void k_ekf(EkfArgs a) {
     if (lane == 0) {
       double x[n], u[m > 0 ? m : 1], xp[n], Gl[n * n];
       for (int c = 0; c < n; ++c) x[c] = mu[c];
-      const double* up = a.U + (long long)b * a.u_bstride + (long long)k * m;
-      for (int c = 0; c < m; ++c) u[c] = up[c];
+      for (int c = 0; c < m; ++c) u[c] = a.U[(long long)b * a.u_bstride + ((long long)k * m + c) * a.es];
       DYN::step(x, u, a.dt, xp, Gl);
       for (int c = 0; c < n; ++c) MP[c] = xp[c];
       for (int c = 0; c < n * n; ++c) G[c] = Gl[c];
@@ -157,17 +158,17 @@ __global__ __launch_bounds__(NWF * 64) void k_ekf(EkfArgs a) {
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    const int nz = a.nz[(long long)b * a.nz_bstride + k];
+    const int nz = a.nz[(long long)b * a.nz_bstride + (long long)k * a.es];
     if (nz > 0 && nz <= MAXP) {
       // ---- measurement rows at mu- (utils/ekf.py:51)
-      const double* zk = a.Z + (long long)b * a.z_bstride + (long long)k * a.nmeas_rows_max;
-      const double* pk = a.PAR + (long long)b * a.par_bstride + (long long)k * a.nmeas_rows_max * q;
+      const long long rk = (long long)k * a.nmeas_rows_max + lane;  // row index within the instance
       if (lane < nz) {
-        double x[n], h, Hr[n];
+        double x[n], h, Hr[n], par[q > 0 ? q : 1];
         for (int c = 0; c < n; ++c) x[c] = MP[c];
-        MEAS::template row<n>(x, pk + lane * q, lane, nz, h, Hr);
+        for (int c = 0; c < q; ++c) par[c] = a.PAR[(long long)b * a.par_bstride + (rk * q + c) * a.es];
+        MEAS::template row<n>(x, par, lane, nz, h, Hr);
         for (int c = 0; c < n; ++c) H[lane * n + c] = Hr[c];
-        E[lane] = zk[lane] - h;
+        E[lane] = a.Z[(long long)b * a.z_bstride + rk * a.es] - h;
       }
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -277,9 +278,8 @@ __global__ __launch_bounds__(256) void k_ekf_lane(EkfArgs a) {
   for (int k = 0; k < a.steps; ++k) {
     // ---- predict: mu- = f(mu, u), S- = G S G^T + Q   (utils/ekf.py:40-45)
     double u[m > 0 ? m : 1], mp[n], G[n * n];
-    const double* up = a.U + (long long)b * a.u_bstride + (long long)k * m;
 #pragma unroll
-    for (int c = 0; c < m; ++c) u[c] = up[c];
+    for (int c = 0; c < m; ++c) u[c] = a.U[(long long)b * a.u_bstride + ((long long)k * m + c) * a.es];
     DYN::step(mu, u, a.dt, mp, G);
     double GS[n * n];
 #pragma unroll
@@ -303,11 +303,12 @@ __global__ __launch_bounds__(256) void k_ekf_lane(EkfArgs a) {
 #pragma unroll
     for (int c = 0; c < n; ++c) mu[c] = mp[c];
     // ---- correct: sequential scalar updates at the linearisation point mu-
-    const int nz = a.nz[(long long)b * a.nz_bstride + k];
+    const int nz = a.nz[(long long)b * a.nz_bstride + (long long)k * a.es];
     if (nz > MAXP) status = 2;
     const int rows = nz <= MAXP ? nz : 0;
-    const double* zk = a.Z + (long long)b * a.z_bstride + (long long)k * a.nmeas_rows_max;
-    const double* pk = a.PAR + (long long)b * a.par_bstride + (long long)k * a.nmeas_rows_max * q;
+    // with batch-innermost inputs (es = batch) consecutive lanes read consecutive words
+    const double* zk = a.Z + (long long)b * a.z_bstride + (long long)k * a.nmeas_rows_max * a.es;
+    const double* pk = a.PAR + (long long)b * a.par_bstride + (long long)k * a.nmeas_rows_max * q * a.es;
     const double* Rk = a.R + (long long)b * a.r_bstride + (long long)k * a.r_sstride;
     // rows in chunks of RCH: all of a chunk's inputs (z, satellite position, R_ii) are
     // loaded before its first update, so a step costs ceil(nz / RCH) memory round
@@ -318,9 +319,9 @@ __global__ __launch_bounds__(256) void k_ekf_lane(EkfArgs a) {
 #pragma unroll
       for (int u = 0; u < RCH; ++u) {
         const int ic = min(i0 + u, rows - 1);
-        zr[u] = zk[ic];
+        zr[u] = zk[ic * a.es];
 #pragma unroll
-        for (int c = 0; c < q; ++c) pr[u][c] = pk[ic * q + c];
+        for (int c = 0; c < q; ++c) pr[u][c] = pk[(ic * q + c) * a.es];
         rr[u] = Rk[ic * a.nmeas_rows_max + ic];
       }
 #pragma unroll
@@ -402,6 +403,11 @@ extern "C" int mhe_ekf_run(const mhe_ekf_dims* dims, int32_t batch, int32_t step
   a.nz_bstride = nz_bstride; a.PAR = PAR; a.par_bstride = par_bstride; a.Q = Q; a.R = R; a.r_bstride = r_bstride;
   a.r_sstride = r_sstride; a.mu_hist = mu_hist; a.S_hist = S_hist; a.status = status;
   a.hist_bi = dims->hist_batch_inner != 0;
+  a.es = 1;
+  if (dims->in_batch_inner) {  // U (steps, m, B), Z (steps, pmax, B), nz (steps, B), PAR (steps, pmax, q, B)
+    a.es = batch;
+    a.u_bstride = a.z_bstride = a.nz_bstride = a.par_bstride = 1;
+  }
   hipStream_t st = (hipStream_t)stream;
   if (dims->dyn_model != MHE_EKF_DYN_GNSS_POS_AND_BIAS || dims->n != 5 || dims->m != 3) return MHE_ERR_MODEL;
   if (dims->q != 3) return MHE_ERR_DIMS;

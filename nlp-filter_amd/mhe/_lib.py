@@ -33,7 +33,7 @@ class MheDims(ctypes.Structure):
 class MheEkfDims(ctypes.Structure):
     _fields_ = [("n", c_i32), ("m", c_i32), ("pmax", c_i32), ("q", c_i32),
                 ("dyn_model", c_i32), ("meas_model", c_i32), ("dt", c_dbl), ("r_diag", c_i32),
-                ("hist_batch_inner", c_i32)]
+                ("hist_batch_inner", c_i32), ("in_batch_inner", c_i32)]
 
 
 class MheLsDims(ctypes.Structure):

@@ -43,7 +43,7 @@ def _ptr(t):
 
 
 def run_batch(dyn_func, meas_func, mu0, S0, U, Z, nz, Q, R, dt, sat_pos, device=None, stream=None,
-              keep_history=True, method="auto"):
+              keep_history=True, method="auto", inputs="batch_outer"):
     """Run B independent filters for T steps in one launch.
 
     mu0 (B,n), S0 (B,n,n), U (B,T,m), Z (B,T,pmax), nz (B,T) valid rows per step
@@ -54,7 +54,10 @@ def run_batch(dyn_func, meas_func, mu0, S0, U, Z, nz, Q, R, dt, sat_pos, device=
 
     method: "lane" (diagonal R: sequential scalar updates, one filter per lane),
     "wave" (any R: one wavefront per filter, augmented Cholesky sweep) or "auto"
-    (lane when every R block is diagonal -- one device-side check)."""
+    (lane when every R block is diagonal -- one device-side check).
+
+    inputs="batch_inner": U, Z, nz, sat_pos are given batch-innermost instead,
+    (T,m,B), (T,pmax,B), (T,B), (T,pmax,3,B) -- the device reads then coalesce."""
     import torch
 
     (did, n, m), (mid, _, q) = models(dyn_func, meas_func)
@@ -67,7 +70,10 @@ def run_batch(dyn_func, meas_func, mu0, S0, U, Z, nz, Q, R, dt, sat_pos, device=
     S = d(S0).clone()
     B = mu.shape[0]
     Zt = d(Z)
-    T, pmax = Zt.shape[1], Zt.shape[2]
+    bi = inputs == "batch_inner"
+    if inputs not in ("batch_outer", "batch_inner"):
+        raise ValueError(f"unknown inputs layout {inputs!r}")
+    T, pmax = (Zt.shape[0], Zt.shape[1]) if bi else (Zt.shape[1], Zt.shape[2])
     if pmax > MAXP:
         raise ValueError(f"at most {MAXP} measurement rows per step")
     Ut = d(U)
@@ -75,8 +81,10 @@ def run_batch(dyn_func, meas_func, mu0, S0, U, Z, nz, Q, R, dt, sat_pos, device=
     Pt = d(sat_pos)
     Rt = d(R)
     Qt = d(Q)
-    if mu.shape != (B, n) or S.shape != (B, n, n) or Ut.shape != (B, T, m) or nzt.shape != (B, T) \
-            or Pt.shape != (B, T, pmax, q) or Qt.shape != (n, n):
+    shapes = ((T, m, B), (T, B), (T, pmax, q, B), (T, pmax, B)) if bi else \
+        ((B, T, m), (B, T), (B, T, pmax, q), (B, T, pmax))
+    if mu.shape != (B, n) or S.shape != (B, n, n) or Ut.shape != shapes[0] or nzt.shape != shapes[1] \
+            or Pt.shape != shapes[2] or Zt.shape != shapes[3] or Qt.shape != (n, n):
         raise ValueError("run_batch: inconsistent shapes")
     if Rt.dim() == 3:
         r_b, r_s = 0, pmax * pmax
@@ -99,7 +107,7 @@ def run_batch(dyn_func, meas_func, mu0, S0, U, Z, nz, Q, R, dt, sat_pos, device=
     else:
         raise ValueError(f"unknown method {method!r}")
     dims = _lib.MheEkfDims(n=n, m=m, pmax=pmax, q=q, dyn_model=did, meas_model=mid, dt=float(dt),
-                           r_diag=int(r_diag), hist_batch_inner=1)
+                           r_diag=int(r_diag), hist_batch_inner=1, in_batch_inner=int(bi))
     lib = _lib.load()
     sh = stream.cuda_stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
     rc = lib.mhe_ekf_run(ctypes.byref(dims), B, T, _ptr(mu), _ptr(S), _ptr(Ut), T * m, _ptr(Zt), T * pmax,

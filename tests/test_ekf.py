@@ -124,15 +124,22 @@ def test_ekf_class_matches_reference_fixture(golden):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("method", ["lane", "wave", "auto"])
-def test_ekf_batch_matches_oracle_per_instance(golden, method):
+@pytest.mark.parametrize("method,inputs", [("lane", "batch_outer"), ("wave", "batch_outer"), ("auto", "batch_outer"),
+                                           ("lane", "batch_inner"), ("wave", "batch_inner")])
+def test_ekf_batch_matches_oracle_per_instance(golden, method, inputs):
     """Both device formulations: sequential scalar updates one filter per lane
-    (diagonal R) and the per-wavefront augmented Cholesky sweep (any R)."""
+    (diagonal R) and the per-wavefront augmented Cholesky sweep (any R); inputs
+    batch-outermost (the reference's per-instance arrays) or batch-innermost."""
     fx = _fixture(golden)
     B = 64
     mu0, S0, U, Z, nz, sat, R = _batch_inputs(fx, B, drop_steps=(5, 6, 30))
-    mh, Sh, mu, S, st = ekf.run_batch(gnss.gnss_pos_and_bias, gnss.multi_pseudorange, mu0, S0, U, Z, nz,
-                                      fx["Q"], R, 1.0, sat, method=method)
+    if inputs == "batch_inner":
+        args = (np.moveaxis(U, 0, -1), np.moveaxis(Z, 0, -1), np.moveaxis(nz, 0, -1))
+        sat_in = np.moveaxis(sat, 0, -1)
+    else:
+        args, sat_in = (U, Z, nz), sat
+    mh, Sh, mu, S, st = ekf.run_batch(gnss.gnss_pos_and_bias, gnss.multi_pseudorange, mu0, S0, *args,
+                                      fx["Q"], R, 1.0, sat_in, method=method, inputs=inputs)
     assert int(st.abs().sum().item()) == 0
     rmu, rS = _oracle_batch(fx, mu0, S0, U, Z, nz, sat)
     emu, eS = _close(mh.cpu().numpy(), Sh.cpu().numpy(), rmu, rS)
