@@ -6,18 +6,18 @@
 //   iterativeLeastSquaresVel  utils/leastsquares.py:45-63  velocity + bias rate
 //                             (one linear solve at the converged position)
 //   runLeastSquares           utils/leastsquares.py:97-141 the per-epoch loop
-// for many logs ("chains") at once.  ONE WAVEFRONT PER TASK, one satellite per
-// lane: each lane forms its geometry row [-(s - x)/|s - x|, 1] and residual;
-// the 4x4 normal equations G^T G dx = G^T drho are wave reductions (DPP /
-// permlane via __shfl_xor), solved by a register Cholesky on every lane.
+// for many logs ("chains") at once.  ONE LANE PER TASK: a lane forms the geometry
+// rows [-(s - x)/|s - x|, 1] and residuals of its epoch's satellites one after the
+// other, accumulates the 4x4 normal equations G^T G dx = G^T drho in registers and
+// solves them by a register Cholesky.
 // For full-column-rank G this is the pinv(G) drho of the reference; results
 // agree to rounding (tests state the tolerance).
 //
 // warm = 1 reproduces the reference's warm start: the default argument x of
 // iterativeLeastSquares is one shared array that every call updates in place,
 // so epoch k starts from epoch k-1's fix (b restarts at 0 every call) -- one
-// wave walks its chain's epochs in order.  warm = 0 solves every epoch
-// independently from x_init (one wave per epoch: all epochs in parallel).
+// lane walks its chain's epochs in order.  warm = 0 solves every epoch
+// independently from x_init (one lane per epoch: all epochs in parallel).
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
@@ -25,8 +25,6 @@
 #include "mhe.h"
 
 namespace mhe_ls {
-
-constexpr int WAVES = 4;  // tasks per workgroup
 
 struct LsArgs {
   int chains, epochs, slots, max_iter, warm, with_vel;
@@ -36,12 +34,6 @@ struct LsArgs {
   double *x_out, *b_out, *v_out, *bd_out, *x_last;
   int32_t* iters;
 };
-
-__device__ __forceinline__ double wsum(double v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
-  return v;
-}
 
 // Solve the 4x4 SPD system A s = v (A packed upper: 00 01 02 03 11 12 13 22 23 33).
 // Returns false on a non-positive pivot (fewer than 4 independent rows).
@@ -73,23 +65,28 @@ __device__ bool solve4(const double* A, const double* v, double* s) {
   return true;
 }
 
-// Normal equations of the rows held by the lanes (g: geometry row, r: residual;
-// inactive lanes pass zeros), then the 4-vector least-squares solution.
-__device__ bool lsq4(const double g[4], double r, double* s) {
-  double A[10], v[4];
+// One task per LANE: a lane walks its log's epochs (warm) or solves one epoch,
+// accumulating the 4x4 normal equations of its satellite rows sequentially in
+// registers -- no cross-lane reductions, 64 tasks per wavefront.
+__device__ __forceinline__ void row_geom(double sp0, double sp1, double sp2, double x0, double x1, double x2,
+                                         double g[4], double& nrm) {
+  const double l0 = sp0 - x0, l1 = sp1 - x1, l2 = sp2 - x2;
+  nrm = sqrt(l0 * l0 + l1 * l1 + l2 * l2);
+  g[0] = -l0 / nrm; g[1] = -l1 / nrm; g[2] = -l2 / nrm; g[3] = 1.0;
+}
+
+__device__ __forceinline__ void accum(double A[10], double v[4], const double g[4], double r) {
   int t = 0;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
 #pragma unroll
-    for (int j = i; j < 4; ++j) A[t++] = wsum(g[i] * g[j]);
-    v[i] = wsum(g[i] * r);
+    for (int j = i; j < 4; ++j) A[t++] += g[i] * g[j];
+    v[i] += g[i] * r;
   }
-  return solve4(A, v, s);
 }
 
-__global__ __launch_bounds__(64 * WAVES) void k_ls(LsArgs a) {
-  const int lane = threadIdx.x & 63;
-  const int task = blockIdx.x * WAVES + (threadIdx.x >> 6);
+__global__ __launch_bounds__(256) void k_ls(LsArgs a) {
+  const int task = blockIdx.x * blockDim.x + threadIdx.x;
   const int ntask = a.warm ? a.chains : a.chains * a.epochs;
   if (task >= ntask) return;
   const int c = a.warm ? task : task / a.epochs;
@@ -99,26 +96,22 @@ __global__ __launch_bounds__(64 * WAVES) void k_ls(LsArgs a) {
   for (int k = k0; k < k1; ++k) {
     const size_t e = (size_t)c * a.epochs + k;
     const int ns = min((int)a.nsat[e], a.slots);  // slots beyond the layout are never read
-    const bool on = lane < ns;
-    double sp0 = 0.0, sp1 = 0.0, sp2 = 0.0, prv = 0.0;
-    if (on) {
-      const double* S = a.sat_pos + (e * a.slots + lane) * 3;
-      sp0 = S[0]; sp1 = S[1]; sp2 = S[2];
-      prv = a.pr[e * a.slots + lane];
-    }
+    const double* S = a.sat_pos + e * a.slots * 3;
+    const double* PR = a.pr + e * a.slots;
     double b = 0.0;
     int it = 0;
-    bool ok = true;
-    for (int i = 0; i < a.max_iter; ++i) {
-      double g[4] = {0.0, 0.0, 0.0, 0.0}, r = 0.0;
-      if (on) {
-        const double l0 = sp0 - x0, l1 = sp1 - x1, l2 = sp2 - x2;
-        const double nrm = sqrt(l0 * l0 + l1 * l1 + l2 * l2);
-        g[0] = -l0 / nrm; g[1] = -l1 / nrm; g[2] = -l2 / nrm; g[3] = 1.0;
-        r = prv - nrm - b;
+    // fewer than 4 rows cannot fix 4 unknowns: flagged (a rank-deficient G^T G would
+    // otherwise leave the last pivot at rounding level, of either sign)
+    bool ok = ns >= 4;
+    for (int i = 0; i < a.max_iter && ok; ++i) {
+      double A[10] = {}, v[4] = {};
+      for (int q = 0; q < ns; ++q) {
+        double g[4], nrm;
+        row_geom(S[3 * q], S[3 * q + 1], S[3 * q + 2], x0, x1, x2, g, nrm);
+        accum(A, v, g, PR[q] - nrm - b);
       }
       double dx[4];
-      if (!lsq4(g, r, dx)) {
+      if (!solve4(A, v, dx)) {
         ok = false;
         break;
       }
@@ -127,29 +120,25 @@ __global__ __launch_bounds__(64 * WAVES) void k_ls(LsArgs a) {
       ++it;
       if (sqrt(dx[0] * dx[0] + dx[1] * dx[1] + dx[2] * dx[2] + dx[3] * dx[3]) < a.tol) break;
     }
-    if (lane == 0) {
-      a.x_out[e * 3] = x0; a.x_out[e * 3 + 1] = x1; a.x_out[e * 3 + 2] = x2;
-      a.b_out[e] = b;
-      a.iters[e] = ok ? it : -1;
-    }
+    a.x_out[e * 3] = x0; a.x_out[e * 3 + 1] = x1; a.x_out[e * 3 + 2] = x2;
+    a.b_out[e] = b;
+    a.iters[e] = ok ? it : -1;
     if (a.with_vel) {  // utils/leastsquares.py:45-63 at the fix just computed
-      double g[4] = {0.0, 0.0, 0.0, 0.0}, r = 0.0;
-      if (on) {
-        const double l0 = sp0 - x0, l1 = sp1 - x1, l2 = sp2 - x2;
-        const double nrm = sqrt(l0 * l0 + l1 * l1 + l2 * l2);
-        g[0] = -l0 / nrm; g[1] = -l1 / nrm; g[2] = -l2 / nrm; g[3] = 1.0;
-        const double* V = a.sat_vel + (e * a.slots + lane) * 3;
-        r = a.pr_rate[e * a.slots + lane] - (V[0] * -g[0] + V[1] * -g[1] + V[2] * -g[2]);
+      const double* V = a.sat_vel + e * a.slots * 3;
+      const double* RR = a.pr_rate + e * a.slots;
+      double A[10] = {}, v[4] = {};
+      for (int q = 0; q < ns; ++q) {
+        double g[4], nrm;
+        row_geom(S[3 * q], S[3 * q + 1], S[3 * q + 2], x0, x1, x2, g, nrm);
+        accum(A, v, g, RR[q] - (V[3 * q] * -g[0] + V[3 * q + 1] * -g[1] + V[3 * q + 2] * -g[2]));
       }
-      double s[4] = {NAN, NAN, NAN, NAN};
-      if (!lsq4(g, r, s) && lane == 0) a.iters[e] = -1;
-      if (lane == 0) {
-        a.v_out[e * 3] = s[0]; a.v_out[e * 3 + 1] = s[1]; a.v_out[e * 3 + 2] = s[2];
-        a.bd_out[e] = s[3];
-      }
+      double sv[4] = {NAN, NAN, NAN, NAN};
+      if (ns < 4 || !solve4(A, v, sv)) a.iters[e] = -1;
+      a.v_out[e * 3] = sv[0]; a.v_out[e * 3 + 1] = sv[1]; a.v_out[e * 3 + 2] = sv[2];
+      a.bd_out[e] = sv[3];
     }
   }
-  if (a.warm && a.x_last && lane == 0) {
+  if (a.warm && a.x_last) {
     a.x_last[3 * c] = x0; a.x_last[3 * c + 1] = x1; a.x_last[3 * c + 2] = x2;
   }
 }
@@ -174,7 +163,7 @@ extern "C" int mhe_ls_run(const mhe_ls_dims* dims, int32_t chains, int32_t epoch
   a.sat_pos = sat_pos; a.pr = pr; a.nsat = nsat; a.sat_vel = sat_vel; a.pr_rate = pr_rate; a.x_init = x_init;
   a.x_out = x_out; a.b_out = b_out; a.v_out = v_out; a.bd_out = bd_out; a.iters = iters_out; a.x_last = x_last;
   const long long ntask = a.warm ? (long long)chains : (long long)chains * epochs;
-  const int blocks = (int)((ntask + WAVES - 1) / WAVES);
-  hipLaunchKernelGGL(k_ls, dim3(blocks), dim3(64 * WAVES), 0, (hipStream_t)stream, a);
+  const int blocks = (int)((ntask + 255) / 256);
+  hipLaunchKernelGGL(k_ls, dim3(blocks), dim3(256), 0, (hipStream_t)stream, a);
   return hipGetLastError() == hipSuccess ? MHE_OK : MHE_ERR_HIP;
 }
