@@ -190,7 +190,7 @@ def main():
                        "parallelism": f"dp{world} (independent trajectories; RCCL broadcast of constants only)"},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None,
-                         "kernel": "mhe::k_gn<DynVanDerPol, MeasFullState<2>, 10, MODE_SOLVE, L2>",
+                         "kernel": "mhe::k_gn<DynVanDerPol, MeasFullState<2>, SLOTS=10, MODE_SOLVE, HUBER=false>",
                          "kernel_ms": kern_ms,
                          "flops_per_launch": fl,
                          "flops_basis": "SURVEY.md 8(d): d^3/3 + 2d^2 + sum_e P^2 nnz(G_e) + 2P^2n^2 + 4Pn^3 "
