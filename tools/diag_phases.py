@@ -10,7 +10,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["MHE_LIB"] = os.path.join(ROOT, "tools", "libmhe_diag.so")
+os.environ["MHE_LIB"] = os.environ.get("MHE_DIAG_LIB", os.path.join(ROOT, "tools", "libmhe_diag.so"))
 sys.path.insert(0, os.path.join(ROOT, "nlp-filter_amd"))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
