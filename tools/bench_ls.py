@@ -60,7 +60,7 @@ res["value"] = res["warm"]["value"]
 by = 8.0 * (12 * 6 + 12 * 2) + 4 + 8.0 * 8 + 4
 res["roofline"] = {"bound": "hbm", "achieved": by * res["value"] / 1e9, "peak": 8000.0, "unit": "GB/s",
                    "frac": by * res["value"] / 1e9 / 8000.0, "bytes_per_fix": by,
-                   "note": "latency-bound: one wavefront per log walks its epochs in order (warm start)"}
+                   "note": "latency-bound: one lane per log walks its epochs in order (warm start); strided per-lane rows"}
 
 nb, t0 = 0, time.perf_counter()
 while time.perf_counter() - t0 < 3.0:
