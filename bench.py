@@ -202,12 +202,20 @@ def main():
         }
         pmc = os.path.join(ROOT, "profiles", "pmc_summary.json")
         if os.path.exists(pmc):
+            # PMC counters come from separate rocprofv3 passes (tools/profile_round.sh);
+            # they are attached only when they measured THIS build of libmhe.so
+            from mhe._lib import lib_digest
             with open(pmc) as f:
                 ps = json.load(f)
-            if ps.get("kernel_sig") == "k_gn<DynVanDerPol" and ps.get("batch") == B and ps.get("iters") == args.iters:
+            same = (ps.get("kernel_sig") == "k_gn<DynVanDerPol" and ps.get("batch") == B
+                    and ps.get("iters") == args.iters)
+            if same and ps.get("lib_sha") == lib_digest():
                 rec["roofline"]["traffic"] = ps["hbm_bytes_per_launch"]
-                rec["roofline"]["traffic_note"] = ps["note"]
+                rec["roofline"]["traffic_note"] = ps["note"] + f"; profiled build {ps['lib_sha']} ({ps['tag']})"
                 rec["roofline"]["mfma_util_pmc"] = ps.get("mfma_util")
+            elif same:
+                rec["roofline"]["traffic_note"] = (f"profiles/pmc_summary.json measured build {ps.get('lib_sha')}, "
+                                                   f"not this libmhe.so ({lib_digest()}): traffic omitted")
         if world == 1 and not args.no_cpu:
             rec["cpu_baseline"] = cpu_baseline(w, args.iters, args.cpu_sample, args.cpu_seconds)
         print(json.dumps(rec))

@@ -54,6 +54,8 @@ extern "C" {
 #define MHE_STATUS_MAX_ITER 1    /* max_iter Gauss-Newton steps taken          */
 #define MHE_STATUS_NOT_SPD 2     /* Cholesky pivot <= 0 (J^T W J not SPD)      */
 #define MHE_STATUS_NONFINITE 3   /* NaN/Inf in the step                        */
+#define MHE_STATUS_BAD_CONSTANTS 4 /* const_buf was not built for these dims (its tag
+                                      differs): nothing was computed, X_out = X0     */
 
 /* dynamics plug-ins (reference nlp/dynamics.py) */
 #define MHE_DYN_SINGLE_INTEGRATOR 1      /* :4-8    n=1  m=1 */
@@ -124,14 +126,23 @@ typedef struct mhe_dims {
   const int32_t* eq_idx;/* HOST pointer, 2*n_eq entries (a, b) into the flattened
                            state vector v = X (P*n, node-major: j*n + c); b = -1
                            means v[a] = 0.  Copied into the constants buffer.     */
+  int32_t force_large;  /* 1: take the large-system path even when the problem fits
+                           the register-resident kernel (parity tests of the two
+                           paths on identical inputs).  The path is a function of
+                           dims alone; mhe_build_constants stamps it (with the
+                           layout-defining dims) into the constants buffer and every
+                           solve checks that stamp on the device.                 */
 } mhe_dims;
 
 /* Dynamics cost (addDynamicsCost, nlp/nlp.py:242-245): */
 #define MHE_COST_L2 0     /* cost_functions.weighted_l2_norm  (cost_functions.py:20-22) */
 #define MHE_COST_HUBER 1  /* cost_functions.pseudo_huber_loss (cost_functions.py:25-31): IRLS
                              weights q_a / sqrt(1 + W_a^2 / delta^2), only diag(Qw) enters */
-/* Bounds (addVarBounds, nlp/nlp.py:314-317) are enforced by projecting every GN
- * step onto the box (projected Gauss-Newton).
+/* Bounds (addVarBounds, nlp/nlp.py:314-317) are enforced by a projected Newton
+ * method on the GN model (Bertsekas 1982): the iterate starts projected onto the
+ * box, each step is the GN step reduced to the free unknowns (epsilon-active set)
+ * followed by an Armijo search along the projection arc; MHE_STATUS_CONVERGED
+ * then means a KKT point of the bounded problem (max|P(X + d) - X| <= tol (1 + max|X|)).
  * Extra variables and equality constraints run on the
  * large-system path: each GN step solves the bordered (KKT) system
  *   [ H    H_xz  C^T ] [dx]   [-g  ]
@@ -142,7 +153,8 @@ typedef struct mhe_dims {
  * therefore met exactly after every step.  Bounds and constraints together are
  * not supported (MHE_ERR_UNSUPPORTED). */
 
-/* Size in bytes of the device constants buffer for `dims` (0 on bad dims). */
+/* Size in bytes of the device constants buffer for `dims` (0 on bad dims).  The
+ * last 256 bytes hold the layout stamp written by mhe_build_constants. */
 size_t mhe_const_bytes(const mhe_dims* dims);
 
 /*
@@ -318,8 +330,10 @@ typedef struct mhe_ls_dims {
  *   sat_pos (C,T,slots,3) ECEF, pr (C,T,slots), nsat (C,T): rows 0..nsat-1 valid
  *   sat_vel (C,T,slots,3), pr_rate (C,T,slots): only with with_vel
  *   x_init (C,3): starting position (b starts at 0 every epoch, as the reference)
- * Outputs: x_out (C,T,3), b_out (C,T), v_out (C,T,3) / bd_out (C,T) with with_vel,
- * iters_out (C,T) GN steps taken (-1: fewer than 4 independent satellites),
+ * Outputs: x_out (C,T,3), b_out (C,T), v_out (C,T,3) / bd_out (C,T) with with_vel
+ * (NaN where the velocity system is singular: velocity failure alone leaves
+ * iters_out untouched), iters_out (C,T) position GN steps taken (-1: fewer than 4
+ * independent satellites for the position fix),
  * x_last (C,3, optional, warm only) the chain's final position (the value the
  * reference's shared default holds afterwards).  Returns MHE_OK or MHE_ERR_*.
  */

@@ -58,7 +58,7 @@ __host__ __device__ inline BigConst big_const_layout(int P, int M, int n, int p,
 }
 
 struct BigWs {  // per-trajectory workspace offsets in doubles
-  size_t H, LT, BV, YV, XE, GEe, Ge, Es, FtE, Vs, FtV, GZe, HZZe, GZVe, BM, ZM, DZ, total;
+  size_t H, LT, BV, YV, XE, GEe, Ge, Es, FtE, Vs, FtV, GZe, HZZe, GZVe, BM, ZM, DZ, ACT, total;
 };
 
 // nz extra variables, nc equality constraints (border of the KKT system)
@@ -87,6 +87,7 @@ __host__ __device__ inline BigWs big_ws_layout(int P, int M, int n, int NT, int 
   W.BM = o;   o = al(o + (size_t)K * dp);                        // border columns [H_xz C^T]
   W.ZM = o;   o = al(o + (size_t)((K + 15) / 16) * 16 * dp);     // H^-1 [H_xz C^T] (16-col panels)
   W.DZ = o;   o = al(o + (size_t)NZX);                           // z step
+  W.ACT = o;  o = al(o + (size_t)dp / 2);                        // bounds: epsilon-active set (int per unknown)
   W.total = o;
   return W;
 }
@@ -109,14 +110,79 @@ struct BigArgs {
   double tol;
   double* ws;      // workspace base
   size_t ws_stride;  // doubles per trajectory
-  int n_bounds;      // projected GN (addVarBounds)
+  int n_bounds;      // addVarBounds: projected Newton (k_big_linesearch)
   int bidx[8];
   double blb[8], bub[8];
   int nz, nc;        // extra variables / equality constraints (f4)
   double* Z;         // (B, nz) current extra variables (Z_out)
+  size_t tag_off;    // layout stamp of the constants buffer (mhe_build_constants)
+  unsigned long long tag;
 };
 
 __device__ __forceinline__ int big_tile_index(int I, int J, int NT) { return J * NT - J * (J - 1) / 2 + (I - J); }
+
+// ------------------------------------------------------------ bounds
+// addVarBounds as the projected Newton method of k_gn_bounded (mhe_gn.hip; oracle
+// gauss_newton_bounded): k_big_resid marks the epsilon-active set, k_big_assemble
+// reduces the active rows / columns of H to their diagonal, k_big_linesearch runs
+// the Armijo search along the projection arc and the stopping test.
+__device__ __forceinline__ void big_box(const BigArgs& a, int c, double& lo, double& hi) {
+  lo = -INFINITY;
+  hi = INFINITY;
+  for (int i = 0; i < a.n_bounds; ++i)
+    if (a.bidx[i] == c) {
+      lo = fmax(lo, a.blb[i]);
+      hi = fmin(hi, a.bub[i]);
+    }
+}
+
+// block max of two values (BIG_NTHREADS threads, red >= 2 BIG_NW doubles), broadcast
+__device__ __forceinline__ void big_max2(double* red, double& x, double& y) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  x = wave_max(x);
+  y = wave_max(y);
+  __syncthreads();
+  if (lane == 0) {
+    red[wave] = x;
+    red[BIG_NW + wave] = y;
+  }
+  __syncthreads();
+  x = red[0];
+  y = red[BIG_NW];
+  for (int w = 1; w < BIG_NW; ++w) {
+    x = fmax(x, red[w]);
+    y = fmax(y, red[BIG_NW + w]);
+  }
+  __syncthreads();
+}
+
+// ACT[c Pp + j] = 1 for the epsilon-active unknowns at X (node-major) with the
+// gradient -BV (component-major); called by every thread of the trajectory's block
+template <int n>
+__device__ void big_active_set(const BigArgs& a, const double* X, const double* BV, int* ACT, double* red) {
+  double w = 0.0, xm = 0.0;
+  for (int t = threadIdx.x; t < a.P * n; t += BIG_NTHREADS) {
+    const int j = t / n, c = t % n;
+    double lo, hi;
+    big_box(a, c, lo, hi);
+    const double x = X[t], g = -BV[c * a.Pp + j];
+    xm = fmax(xm, fabs(x));
+    if (lo > -INFINITY || hi < INFINITY) w = fmax(w, fabs(x - fmin(fmax(x - g, lo), hi)));
+  }
+  big_max2(red, w, xm);
+  const double eps = fmin(1e-6 * (1.0 + xm), w);  // EPS_ACT
+  for (int t = threadIdx.x; t < n * a.Pp; t += BIG_NTHREADS) {
+    const int c = t / a.Pp, j = t % a.Pp;
+    int act = 0;
+    if (j < a.P) {
+      double lo, hi;
+      big_box(a, c, lo, hi);
+      const double x = X[j * n + c], g = -BV[t];
+      act = (lo > -INFINITY || hi < INFINITY) && ((x <= lo + eps && g > 0.0) || (x >= hi - eps && g < 0.0));
+    }
+    ACT[t] = act;
+  }
+}
 
 // ------------------------------------------------------------ residuals
 template <class DYN, class MEAS>
@@ -124,6 +190,7 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_resid(BigArgs a, int final
   constexpr int n = DYN::n, m = DYN::m, p = MEAS::p, q = MEAS::q;
   const int b = blockIdx.x;
   if (!final_pass && a.state[b] != BIG_RUNNING) return;
+  if (a.state[b] == MHE_STATUS_BAD_CONSTANTS) return;
   const BigConst CL = big_const_layout(a.P, a.M, n, p, a.nc);
   const BigWs WL = big_ws_layout(a.P, a.M, n, a.NT, a.nz, a.nc);
   double* ws = a.ws + (size_t)b * a.ws_stride;
@@ -139,7 +206,7 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_resid(BigArgs a, int final
   const int E = a.M > 0 ? *(const int*)(a.cbuf + CL.ne) : 0;
   const int Mr = a.M > 0 ? a.M : 1;
   const double* X = a.X + (size_t)b * a.P * n;
-  __shared__ double red[BIG_NW];
+  __shared__ double red[2 * BIG_NW];
   double cost = 0.0;
   // interpolated states at the epochs: x_e = sum_j Phi_E[e][j] X_j
   for (int e = threadIdx.x; e < E; e += BIG_NTHREADS) {
@@ -324,6 +391,7 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_resid(BigArgs a, int final
     for (int w = 0; w < BIG_NW; ++w) c += red[w];
     a.cost[b] = c;
   }
+  if (a.n_bounds > 0 && !final_pass) big_active_set<n>(a, X, ws + WL.BV, (int*)(ws + WL.ACT), red);
 }
 
 // ------------------------------------------------------------ assembly
@@ -435,6 +503,11 @@ __global__ __launch_bounds__(256, 4) void k_big_assemble(BigArgs a) {
             if (a.has_prior && j == 0 && l == 0) v += Pw[ca * n + cb];
           } else {
             v = (I == J && tr == tc) ? 1.0 : 0.0;
+          }
+          if (a.n_bounds > 0) {  // active rows / columns reduced to the diagonal (projected Newton)
+            const int* ACT = (const int*)(ws + WL.ACT);
+            const int gr = 16 * I + tr, gc = 16 * J + tc;
+            if ((ACT[gr] | ACT[gc]) && gr != gc) v = 0.0;
           }
           tile[tr * 16 + tc] = v;
         }
@@ -871,6 +944,7 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_border(BigArgs a) {
 }
 
 // ------------------------------------------------------------ update
+// Unbounded problems (bounded ones run k_big_linesearch instead).
 template <int n>
 __global__ __launch_bounds__(256) void k_big_update(BigArgs a) {
   const int b = blockIdx.x;
@@ -891,13 +965,7 @@ __global__ __launch_bounds__(256) void k_big_update(BigArgs a) {
     const int j = t / n, c = t % n;
     const double dv = YV[c * a.Pp + j];
     if (!isfinite(dv)) fin = 1.0;
-    double step = dv;
-    for (int i = 0; i < a.n_bounds; ++i)
-      if (a.bidx[i] == c) {
-        const double xv = X[t] + dv, xc = fmin(fmax(xv, a.blb[i]), a.bub[i]);
-        if (xc != xv) step = xc - X[t];
-      }
-    dmax = fmax(dmax, fabs(step));
+    dmax = fmax(dmax, fabs(dv));
   }
   dmax = wave_max(dmax);
   fin = wave_max(fin);
@@ -921,9 +989,7 @@ __global__ __launch_bounds__(256) void k_big_update(BigArgs a) {
   }
   for (int t = threadIdx.x; t < a.P * n; t += 256) {
     const int j = t / n, c = t % n;
-    double xv = X[t] + YV[c * a.Pp + j];
-    for (int i = 0; i < a.n_bounds; ++i)
-      if (a.bidx[i] == c) xv = fmin(fmax(xv, a.blb[i]), a.bub[i]);
+    const double xv = X[t] + YV[c * a.Pp + j];
     X[t] = xv;
     xmax = fmax(xmax, fabs(xv));
   }
@@ -937,11 +1003,197 @@ __global__ __launch_bounds__(256) void k_big_update(BigArgs a) {
   }
 }
 
-__global__ void k_big_init(int batch, int* state, int* iters) {
+// Objective at X (node-major, any memory; the extra variables z of mixed rows are
+// not supported with bounds): the sums of k_big_resid without Jacobians.  Every
+// thread of the block calls it; returns the block total in every thread.
+template <class MEAS, int n, bool = MEAS::MIXED>
+struct MeasArgLen {  // length of the argument vector h reads: x (n), or [x ; z] for mixed rows
+  static constexpr int v = n;
+};
+template <class MEAS, int n>
+struct MeasArgLen<MEAS, n, true> {
+  static constexpr int v = MEAS::NA;
+};
+
+template <class DYN, class MEAS>
+__device__ double big_cost(const BigArgs& a, const double* X, int b, double* red) {
+  constexpr int n = DYN::n, m = DYN::m, p = MEAS::p, q = MEAS::q, NAX = MeasArgLen<MEAS, n>::v;
+  const BigConst CL = big_const_layout(a.P, a.M, n, p, a.nc);
+  const double* Dt = (const double*)(a.cbuf + CL.Dt);
+  const double* cw = (const double*)(a.cbuf + CL.cw);
+  const double* Qw = (const double*)(a.cbuf + CL.Qw);
+  const double* Pw = (const double*)(a.cbuf + CL.Pw);
+  const double* Rw = (const double*)(a.cbuf + CL.Rw);
+  const double* PhiET = (const double*)(a.cbuf + CL.PhiET);
+  const int* erow = (const int*)(a.cbuf + CL.erow);
+  const int E = a.M > 0 ? *(const int*)(a.cbuf + CL.ne) : 0;
+  const int Mr = a.M > 0 ? a.M : 1;
+  double cost = 0.0;
+  for (int k = threadIdx.x; k < a.P; k += BIG_NTHREADS) {
+    double dx[n], xk[n], uk[m > 0 ? m : 1], f[n], F[n * n];
+    for (int c = 0; c < n; ++c) dx[c] = 0.0;
+    for (int j = 0; j < a.P; ++j) {
+      const double dv = Dt[(size_t)j * a.P + k];
+      for (int c = 0; c < n; ++c) dx[c] += dv * X[j * n + c];
+    }
+    for (int c = 0; c < n; ++c) xk[c] = X[k * n + c];
+    if (m > 0) {
+      const double* Up = a.U + (long long)b * a.ustride + (long long)k * m;
+      for (int c = 0; c < m; ++c) uk[c] = Up[c];
+    }
+    DYN::eval(xk, uk, f, F);
+    double W[n];
+    for (int c = 0; c < n; ++c) W[c] = a.alpha * dx[c] - f[c];
+    const double ck = cw[k];
+    for (int r = 0; r < n; ++r) {
+      double s = 0.0;
+      for (int c = 0; c < n; ++c) s += Qw[r * n + c] * W[c];
+      cost += W[r] * (ck * s);
+    }
+  }
+  for (int e = threadIdx.x; e < E; e += BIG_NTHREADS) {
+    double xe[NAX];
+    for (int c = 0; c < NAX; ++c) xe[c] = 0.0;
+    for (int j = 0; j < a.P; ++j) {
+      const double ph = PhiET[(size_t)j * Mr + e];
+      for (int c = 0; c < n; ++c) xe[c] += ph * X[j * n + c];
+    }
+    for (int i = erow[e]; i < erow[e + 1]; ++i) {
+      if constexpr (MEAS::MIXED) {
+        const double* PR = a.PAR + (long long)b * a.pstride + (long long)i * q;
+        const double R = Rw[i];
+        if (R == 0.0) continue;
+        double h, Gr[NAX];
+        MEAS::eval(xe, PR, 0, h, Gr);
+        const double ev = a.Y[(long long)b * a.M + i] - h;
+        cost += ev * (R * ev);
+      } else {
+        double par[q > 0 ? q : 1];
+        if (q > 0) {
+          const double* PR = a.PAR + (long long)b * a.pstride + (long long)i * q;
+          for (int c = 0; c < q; ++c) par[c] = PR[c];
+        }
+        const double* R = Rw + (size_t)i * p * p;
+        if (masked_row<p>(R)) continue;
+        double h[p], Hm[p * n];
+        MEAS::eval(xe, par, a.idx, h, Hm);
+        const double* yi = a.Y + ((long long)b * a.M + i) * p;
+        double ev[p];
+        for (int r = 0; r < p; ++r) ev[r] = yi[r] - h[r];
+        for (int r = 0; r < p; ++r) {
+          double s = 0.0;
+          for (int c = 0; c < p; ++c) s += R[r * p + c] * ev[c];
+          cost += ev[r] * s;
+        }
+      }
+    }
+  }
+  if (a.has_prior && threadIdx.x == 0) {
+    for (int r = 0; r < n; ++r) {
+      double t2 = 0.0;
+      for (int c = 0; c < n; ++c) t2 += Pw[r * n + c] * (X[c] - a.x0[(long long)b * n + c]);
+      cost += (X[r] - a.x0[(long long)b * n + r]) * t2;
+    }
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  cost = wave_sum(cost);
+  __syncthreads();
+  if (lane == 0) red[wave] = cost;
+  __syncthreads();
+  double c = 0.0;
+  for (int w = 0; w < BIG_NW; ++w) c += red[w];
+  __syncthreads();
+  return c;
+}
+
+// Bounded problems: replaces k_big_update.  Stationarity measure s = P(X + d) - X,
+// Armijo search along P(X + a d) (trial iterates in LDS, cost by big_cost), X <-
+// accepted trial, convergence max|s| <= tol (1 + max|X|).  Constants as k_gn_bounded.
+template <class DYN, class MEAS>
+__global__ __launch_bounds__(BIG_NTHREADS) void k_big_linesearch(BigArgs a) {
+  constexpr int n = DYN::n;
+  const int b = blockIdx.x;
+  if (a.state[b] != BIG_RUNNING) return;
+  const BigWs WL = big_ws_layout(a.P, a.M, n, a.NT, a.nz, a.nc);
+  const double* ws = a.ws + (size_t)b * a.ws_stride;
+  const double* YV = ws + WL.YV;
+  const double* BV = ws + WL.BV;
+  const int* ACT = (const int*)(ws + WL.ACT);
+  double* X = a.X + (size_t)b * a.P * n;
+  extern __shared__ __attribute__((aligned(16))) double xt[];  // trial iterate (P, n)
+  __shared__ double red[2 * BIG_NW];
+  double smax = 0.0, fin = 0.0;
+  for (int t = threadIdx.x; t < a.P * n; t += BIG_NTHREADS) {
+    const int j = t / n, c = t % n;
+    double lo, hi;
+    big_box(a, c, lo, hi);
+    const double x = X[t], dv = YV[c * a.Pp + j];
+    if (!isfinite(dv)) fin = 1.0;
+    smax = fmax(smax, fabs(fmin(fmax(x + dv, lo), hi) - x));
+  }
+  big_max2(red, smax, fin);
+  if (fin != 0.0) {
+    if (threadIdx.x == 0) a.state[b] = MHE_STATUS_NONFINITE;
+    return;
+  }
+  const double cost0 = a.cost[b];  // k_big_resid at X
+  double alpha = 1.0;
+  for (int ls = 0;;) {
+    double pred = 0.0;
+    for (int t = threadIdx.x; t < a.P * n; t += BIG_NTHREADS) {
+      const int j = t / n, c = t % n;
+      double lo, hi;
+      big_box(a, c, lo, hi);
+      const int u = c * a.Pp + j;
+      const double x = X[t], dv = YV[u], g = -BV[u];
+      const double xv = fmin(fmax(x + alpha * dv, lo), hi);
+      pred += ACT[u] ? g * (xv - x) : alpha * g * dv;
+      xt[t] = xv;
+    }
+    __syncthreads();
+    const double ct = big_cost<DYN, MEAS>(a, xt, b, red);
+    pred = wave_sum(pred);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = pred;
+    __syncthreads();
+    pred = 0.0;
+    for (int w = 0; w < BIG_NW; ++w) pred += red[w];
+    __syncthreads();
+    ++ls;
+    if (ct <= cost0 + 2.0 * 1e-4 * pred + 1e-12 * fabs(cost0) || ls >= 30) break;  // ARMIJO_SIGMA, COST_SLACK, LS_MAX
+    alpha *= 0.5;
+  }
+  double xn = 0.0, z = 0.0;
+  for (int t = threadIdx.x; t < a.P * n; t += BIG_NTHREADS) {
+    X[t] = xt[t];
+    xn = fmax(xn, fabs(xt[t]));
+  }
+  big_max2(red, xn, z);
+  if (threadIdx.x == 0) {
+    a.iters[b] += 1;
+    if (smax <= a.tol * (1.0 + xn)) a.state[b] = MHE_STATUS_CONVERGED;
+  }
+}
+
+// X <- P(X) (bounded problems: the projected Newton method starts inside the box)
+template <int n>
+__global__ void k_big_project(BigArgs a, int batch) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (size_t)batch * a.P * n || a.state[t / ((size_t)a.P * n)] != BIG_RUNNING) return;
+  double lo, hi;
+  big_box(a, (int)(t % n), lo, hi);
+  a.X[t] = fmin(fmax(a.X[t], lo), hi);
+}
+
+// Every trajectory starts RUNNING -- or, when the constants buffer's stamp does not
+// match these dims, BAD_CONSTANTS: then no kernel of the solve touches the constants
+// (X_out keeps X0, cost NaN).
+__global__ void k_big_init(BigArgs a, int batch) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b < batch) {
-    state[b] = BIG_RUNNING;
-    iters[b] = 0;
+    const bool ok = *(const unsigned long long*)(a.cbuf + a.tag_off) == a.tag;
+    a.state[b] = ok ? BIG_RUNNING : MHE_STATUS_BAD_CONSTANTS;
+    a.iters[b] = 0;
+    if (!ok) a.cost[b] = NAN;
   }
 }
 

@@ -72,7 +72,7 @@ __host__ __device__ inline ConstLayout const_layout(int P, int M, int n, int p, 
 }
 
 struct SmemLayout {  // offsets in doubles
-  int Xs, Vs, FtV, Es, FtE, GE, G, LAM, BV, YV, PB, DT, RED, total;
+  int Xs, Vs, FtV, Es, FtE, GE, G, LAM, BV, YV, PB, DT, RED, XO, ACT, total;
 };
 
 __host__ __device__ inline int rnd2(int x) { return (x + 1) & ~1; }  // keep 16-B alignment
@@ -80,7 +80,7 @@ __host__ __device__ inline int rnd2(int x) { return (x + 1) & ~1; }  // keep 16-
 constexpr int DTS = 272;  // diagonal-tile stride: A_kk row-major (256), then L_kk^-T with row stride 17
 constexpr int LIS = 17;   // row stride of L_kk^-T (conflict-free row and column reads)
 
-__host__ __device__ inline SmemLayout smem_layout(int P, int M, int n, int NT, bool nonlinear) {
+__host__ __device__ inline SmemLayout smem_layout(int P, int M, int n, int NT, bool nonlinear, bool bounded = false) {
   SmemLayout S;
   int o = 0;
   const int dp = 16 * NT;
@@ -97,6 +97,10 @@ __host__ __device__ inline SmemLayout smem_layout(int P, int M, int n, int NT, b
   S.PB = o;   o += (NT - 1) * 256;      // block row k of U (tiles U_kb, b > k), register order
   S.DT = o;   o += NT * DTS;            // diagonal blocks
   S.RED = o;  o += 4 * NW + 8;
+  // bounded problems only (projected Newton, k_gn<..., BOUNDED>): the iterate the
+  // line search starts from, and the epsilon-active set (one int per unknown)
+  S.XO = o;   o += bounded ? rnd2(P * n) : 0;
+  S.ACT = o;  o += bounded ? dp / 2 : 0;
   S.total = o;
   return S;
 }
@@ -126,7 +130,9 @@ struct GnArgs {
   double* dout;
   unsigned long long* dbg;  // MHE_DIAG builds only: per-phase cycle sums
   double huber_delta;       // MHE_COST_HUBER only
-  int n_bounds;             // projected GN: components bidx[i] clipped to [blb, bub]
+  int n_bounds;             // addVarBounds: components bidx[i] in [blb, bub] (k_gn_bounded)
+  size_t tag_off;           // layout stamp of the constants buffer (mhe_build_constants)
+  unsigned long long tag;
   int bidx[8];
   double blb[8], bub[8];
 };
@@ -711,9 +717,13 @@ __device__ __forceinline__ double h_element(const GnArgs& a, const double* Phi, 
 // Cc, DA = a D_lj and DB = a D_jl are stored per tile element in the MFMA
 // C-layout, so each is one coalesced 512-B load per register.  Off-diagonal
 // tiles go to the accumulator slots, diagonal tiles (owner wave J % NW) to LDS.
-template <class DYN, class MEAS, int SLOTS, bool HUBER = false>
+// BOUNDED (projected Newton, k_gn_bounded): rows and columns of the epsilon-active
+// unknowns (ACT) are replaced by their diagonal entries -- the reduced GN system on
+// the free unknowns, a diagonally scaled gradient step on the active ones.
+template <class DYN, class MEAS, int SLOTS, bool HUBER = false, bool BOUNDED = false>
 __device__ __forceinline__ void build_tiles(const GnArgs& a, const ConstLayout& CL, const SmemLayout& SL, double* sm,
                                             d4 (&acc)[SLOTS], int wave, int lane, int stab) {
+  const int* ACT = (const int*)(sm + SL.ACT);
   const double* Dm = (const double*)(a.cbuf + CL.D);
   const double* LAM = sm + SL.LAM;
   const double* Cc = (const double*)(a.cbuf + CL.Cc);
@@ -753,6 +763,7 @@ __device__ __forceinline__ void build_tiles(const GnArgs& a, const ConstLayout& 
           const int src = (((lane & 15) >> 1) * 8 + (lane >> 5) + 2 * r) * 4;
           acc[s][r] = -h_element<DYN, MEAS, HUBER>(a, Phi, Es, FtE, G, Cc[off + 64 * r], bpermute_d(src, dac),
                                                    bpermute_d(src, dbc), row, col, Dm, LAM);
+          if (BOUNDED && (ACT[row] | ACT[col])) acc[s][r] = 0.0;
         }
       } else {
 #pragma unroll
@@ -760,6 +771,7 @@ __device__ __forceinline__ void build_tiles(const GnArgs& a, const ConstLayout& 
           const int row = 16 * J + (lane >> 4) + 4 * r;
           acc[s][r] = -h_element<DYN, MEAS, HUBER>(a, Phi, Es, FtE, G, Cc[off + 64 * r], DA[off + 64 * r],
                                                    DB[off + 64 * r], row, col, Dm, LAM);
+          if (BOUNDED && (ACT[row] | ACT[col])) acc[s][r] = 0.0;
         }
       }
     }
@@ -788,8 +800,9 @@ __device__ __forceinline__ void build_tiles(const GnArgs& a, const ConstLayout& 
         da = DA[off + 64 * r];
         db = DB[off + 64 * r];
       }
-      DT[J * DTS + tr * 16 + (lane & 15)] = -h_element<DYN, MEAS, HUBER>(a, Phi, Es, FtE, G, Cc[off + 64 * r], da,
-                                                                         db, 16 * J + tr, col, Dm, LAM);
+      double v = -h_element<DYN, MEAS, HUBER>(a, Phi, Es, FtE, G, Cc[off + 64 * r], da, db, 16 * J + tr, col, Dm, LAM);
+      if (BOUNDED && (ACT[16 * J + tr] | ACT[col]) && 16 * J + tr != col) v = 0.0;
+      DT[J * DTS + tr * 16 + (lane & 15)] = v;
     }
   }
 }
@@ -1159,6 +1172,23 @@ __device__ __forceinline__ void backward(const GnArgs& a, const SmemLayout& SL, 
   }
 }
 
+// The constants buffer ends with a stamp of the dims that define its layout
+// (const_tag); a solve whose dims disagree computes nothing and reports
+// MHE_STATUS_BAD_CONSTANTS (no out-of-layout reads).
+__device__ __forceinline__ bool tag_ok(const GnArgs& a) {
+  return *(const unsigned long long*)(a.cbuf + a.tag_off) == a.tag;
+}
+
+__device__ void bad_constants(const GnArgs& a, int b, int mode) {
+  if (mode == MODE_SOLVE)
+    for (int t = threadIdx.x; t < a.d; t += blockDim.x) a.Xout[(size_t)b * a.d + t] = a.X0[(size_t)b * a.d + t];
+  if (threadIdx.x == 0) {
+    if (mode != MODE_ASSEMBLE) a.status[b] = MHE_STATUS_BAD_CONSTANTS;
+    if (mode == MODE_SOLVE) a.iters[b] = 0;
+    if (mode != MODE_LINSOLVE) a.cost[b] = NAN;
+  }
+}
+
 #include "mhe_big.h"
 
 // Inside the Gauss-Newton loop every phase recomputes the layouts (and the
@@ -1191,6 +1221,10 @@ __global__ __launch_bounds__(NTHREADS, NW / 2) void k_gn(GnArgs a) {  // 2nd arg
   d4 acc[SLOTS];
 #pragma unroll
   for (int s = 0; s < SLOTS; ++s) acc[s] = d4{0.0, 0.0, 0.0, 0.0};
+  if (!tag_ok(a)) {  // constants built for other dims: compute nothing
+    bad_constants(a, b, mode);
+    return;
+  }
 
   __syncthreads();
   if constexpr (mode == MODE_LINSOLVE) {
@@ -1268,34 +1302,21 @@ __global__ __launch_bounds__(NTHREADS, NW / 2) void k_gn(GnArgs a) {  // 2nd arg
     }
     backward<SLOTS>(FA, FSL, sm, acc, wave, lane, stab);
     DIAG_MARK(4);
-    // X += delta, projected onto the bounds (addVarBounds); the convergence test uses
-    // |delta| for unclipped components and the actual move for clipped ones.  A
-    // non-finite delta is flagged as an infinite step (NONFINITE, X untouched).
+    // X += delta (bounded problems run k_gn_bounded).  A non-finite delta is flagged
+    // as an infinite step (NONFINITE, X untouched).
     double dmax = 0.0, xmax = 0.0;
     const int tid_u = opaque_tid();
     for (int t = tid_u; t < a.d; t += NTHREADS) {
       const double dv = DV[t];
-      double xv = Xs[t] + dv, step = dv;
-      for (int i = 0; i < a.n_bounds; ++i)
-        if (a.bidx[i] == t % n) {
-          const double xc = fmin(fmax(xv, a.blb[i]), a.bub[i]);
-          if (xc != xv) step = xc - Xs[t];
-          xv = xc;
-        }
-      dmax = isfinite(dv) ? fmax(dmax, fabs(step)) : INFINITY;
-      xmax = fmax(xmax, fabs(xv));
+      dmax = isfinite(dv) ? fmax(dmax, fabs(dv)) : INFINITY;
+      xmax = fmax(xmax, fabs(Xs[t] + dv));
     }
     block_reduce2(RED, dmax, xmax, true);
     if (dmax == INFINITY) {
       status = MHE_STATUS_NONFINITE;
       break;
     }
-    for (int t = tid_u; t < a.d; t += NTHREADS) {
-      double xv = Xs[t] + DV[t];
-      for (int i = 0; i < a.n_bounds; ++i)
-        if (a.bidx[i] == t % n) xv = fmin(fmax(xv, a.blb[i]), a.bub[i]);
-      Xs[t] = xv;
-    }
+    for (int t = tid_u; t < a.d; t += NTHREADS) Xs[t] = Xs[t] + DV[t];
     __syncthreads();
     ++it;
     if (dmax <= a.tol * (1.0 + xmax)) {
@@ -1330,6 +1351,181 @@ done:
     a.status[b] = status;
   }
 }
+// ------------------------------------------------------------ bounds
+// addVarBounds (nlp/nlp.py:314-317: lb <= x[idx] <= ub at every node) as a
+// projected Newton method on the GN model (Bertsekas 1982), restated in
+// oracle/gn.py:gauss_newton_bounded -- same constants, same decisions:
+//   X <- P(X0); per iteration at X (g = J^T W r, half the cost gradient):
+//   eps = min(EPS_ACT (1 + max|X|), max_bounded |X - P(X - g)|)
+//   active: bounded, within eps of a bound, gradient pointing out of the box
+//   d = -Ht^-1 g   (Ht: H with the active rows / columns reduced to the diagonal)
+//   s = P(X + d) - X  (stationarity measure: 0 exactly at a KKT point)
+//   Armijo along the projection arc X(a) = P(X + a d), a = 1, 1/2, ... (LS_MAX trials):
+//     cost(X(a)) <= cost(X) + 2 sigma [sum_free a g d + sum_act g (X(a) - X)] + slack |cost(X)|
+//   converged when max|s| <= tol (1 + max|X(a)|).
+// Limit points are KKT points of the bound-constrained problem (plain clipping of
+// the GN step is not: its fixed points need not be).
+constexpr double EPS_ACT = 1e-6;
+constexpr double ARMIJO_SIGMA = 1e-4;
+constexpr int LS_MAX = 30;
+constexpr double COST_SLACK = 1e-12;
+
+// box of state component c: intersection of every addVarBounds entry for it
+__device__ __forceinline__ void comp_box(const GnArgs& a, int c, double& lo, double& hi) {
+  lo = -INFINITY;
+  hi = INFINITY;
+  for (int i = 0; i < a.n_bounds; ++i)
+    if (a.bidx[i] == c) {
+      lo = fmax(lo, a.blb[i]);
+      hi = fmin(hi, a.bub[i]);
+    }
+}
+
+// prior cost (X_0 - x0)^T Pw (X_0 - x0), same operation order as grad_phase
+template <int n>
+__device__ __forceinline__ double prior_cost(const GnArgs& a, const double* Pw, const double* Xs, int b) {
+  double r0[n], cost = 0.0;
+#pragma unroll
+  for (int c = 0; c < n; ++c) r0[c] = Xs[c] - a.x0[(long long)b * n + c];
+#pragma unroll
+  for (int r = 0; r < n; ++r) {
+    double t2 = 0.0;
+#pragma unroll
+    for (int c = 0; c < n; ++c) t2 += Pw[r * n + c] * r0[c];
+    cost += r0[r] * t2;
+  }
+  return cost;
+}
+
+#define FSLB smem_layout(opaque_s(a.P), opaque_s(a.M), n, opaque_s(a.NT), !MEAS::LINEAR, true)
+
+template <class DYN, class MEAS, int SLOTS, bool HUBER = false>
+__global__ __launch_bounds__(NTHREADS, NW / 2) void k_gn_bounded(GnArgs a) {
+  constexpr int n = DYN::n;
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  const SmemLayout SL = smem_layout(a.P, a.M, n, a.NT, !MEAS::LINEAR, true);
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int b = blockIdx.x;
+  const int stab = make_slot_table(wave, lane, a.NT);
+  double* Xs = sm + SL.Xs;
+  double* XO = sm + SL.XO;
+  int* ACT = (int*)(sm + SL.ACT);
+  const double* BV = sm + SL.BV;  // -g at the current iterate
+  const double* DV = sm + SL.YV;  // step after backward()
+  double* RED = sm + SL.RED;
+  if (threadIdx.x == 0) *(int*)(sm + SL.RED + 4 * NW) = 0;  // NOT_SPD flag
+  d4 acc[SLOTS];
+#pragma unroll
+  for (int s = 0; s < SLOTS; ++s) acc[s] = d4{0.0, 0.0, 0.0, 0.0};
+  if (!tag_ok(a)) {
+    bad_constants(a, b, MODE_SOLVE);
+    return;
+  }
+  for (int t = threadIdx.x; t < a.d; t += NTHREADS) {
+    double lo, hi;
+    comp_box(a, t % n, lo, hi);
+    Xs[t] = fmin(fmax(a.X0[(size_t)b * a.d + t], lo), hi);  // X <- P(X0)
+  }
+  for (int t = threadIdx.x; t < 16 * a.NT; t += NTHREADS) ACT[t] = 0;
+  __syncthreads();
+  double cost = node_meas_phase<DYN, MEAS, HUBER>(FA, FCL, FSLB, sm, opaque_s(b));
+  __syncthreads();
+  cost += grad_phase<DYN>(FA, FCL, FSLB, sm, opaque_s(b));
+  {
+    double z = 0.0;
+    block_reduce2(RED, cost, z, false);
+  }
+  int status = MHE_STATUS_MAX_ITER;
+  int it = 0;
+  DIAG_DECL
+  for (;;) {
+    if (it >= a.max_iter) break;
+    // epsilon-active set
+    double w = 0.0, xm = 0.0;
+    for (int t = threadIdx.x; t < a.d; t += NTHREADS) {
+      double lo, hi;
+      comp_box(a, t % n, lo, hi);
+      const double x = Xs[t], g = -BV[t];
+      xm = fmax(xm, fabs(x));
+      if (lo > -INFINITY || hi < INFINITY) w = fmax(w, fabs(x - fmin(fmax(x - g, lo), hi)));
+    }
+    block_reduce2(RED, w, xm, true);
+    const double eps = fmin(EPS_ACT * (1.0 + xm), w);
+    for (int t = threadIdx.x; t < a.d; t += NTHREADS) {
+      double lo, hi;
+      comp_box(a, t % n, lo, hi);
+      const double x = Xs[t], g = -BV[t];
+      ACT[t] = (lo > -INFINITY || hi < INFINITY) && ((x <= lo + eps && g > 0.0) || (x >= hi - eps && g < 0.0));
+    }
+    __syncthreads();
+    build_tiles<DYN, MEAS, SLOTS, HUBER, true>(FA, FCL, FSLB, sm, acc, wave, lane, stab);
+    __syncthreads();
+    const bool ok = factor_forward<SLOTS>(FA, FSLB, sm, acc, wave, lane, stab, DIAG_FARGS);
+    if (!ok) {
+      status = MHE_STATUS_NOT_SPD;
+      break;
+    }
+    backward<SLOTS>(FA, FSLB, sm, acc, wave, lane, stab);
+    // stationarity measure s = P(X + d) - X; keep X for the line search
+    double smax = 0.0, fin = 0.0;
+    for (int t = threadIdx.x; t < a.d; t += NTHREADS) {
+      double lo, hi;
+      comp_box(a, t % n, lo, hi);
+      const double x = Xs[t], dv = DV[t];
+      XO[t] = x;
+      if (!isfinite(dv)) fin = 1.0;
+      smax = fmax(smax, fabs(fmin(fmax(x + dv, lo), hi) - x));
+    }
+    block_reduce2(RED, smax, fin, true);
+    if (fin != 0.0) {
+      status = MHE_STATUS_NONFINITE;  // X untouched
+      break;
+    }
+    // Armijo search along the projection arc
+    double alpha = 1.0, ct = 0.0;
+    for (int ls = 0;;) {
+      double pred = 0.0;
+      for (int t = threadIdx.x; t < a.d; t += NTHREADS) {
+        double lo, hi;
+        comp_box(a, t % n, lo, hi);
+        const double x = XO[t], dv = DV[t], g = -BV[t];
+        const double xt = fmin(fmax(x + alpha * dv, lo), hi);
+        pred += ACT[t] ? g * (xt - x) : alpha * g * dv;
+        Xs[t] = xt;
+      }
+      __syncthreads();
+      ct = node_meas_phase<DYN, MEAS, HUBER>(FA, FCL, FSLB, sm, opaque_s(b));
+      if (threadIdx.x == 0 && a.has_prior)
+        ct += prior_cost<n>(a, (const double*)(a.cbuf + FCL.Pw), Xs, b);
+      block_reduce2(RED, ct, pred, false);
+      ++ls;
+      if (ct <= cost + 2.0 * ARMIJO_SIGMA * pred + COST_SLACK * fabs(cost) || ls >= LS_MAX) break;
+      alpha *= 0.5;
+    }
+    cost = ct;
+    ++it;
+    double xn = 0.0, z = 0.0;
+    for (int t = threadIdx.x; t < a.d; t += NTHREADS) xn = fmax(xn, fabs(Xs[t]));
+    block_reduce2(RED, xn, z, true);
+    if (smax <= a.tol * (1.0 + xn)) {
+      status = MHE_STATUS_CONVERGED;
+      break;
+    }
+    // gradient at the accepted iterate (its node / row quantities are in LDS from the
+    // line search's last evaluation)
+    grad_phase<DYN>(FA, FCL, FSLB, sm, opaque_s(b));
+    __syncthreads();
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < a.d; t += NTHREADS) a.Xout[(size_t)b * a.d + t] = Xs[t];
+  if (threadIdx.x == 0) {
+    a.cost[b] = cost;
+    a.iters[b] = it;
+    a.status[b] = status;
+  }
+}
+#undef FSLB
 #undef FA
 #undef FCL
 #undef FSL
@@ -1458,14 +1654,13 @@ bool meas_info(int id, int n, int& p, int& q, bool& linear) {
   return false;
 }
 
-// Register-resident path iff the node-major padded system fits MAX_NT tiles.
-// MHE_FORCE_BIG=1 (tests only) routes every problem through the large-system
-// path so both paths can be compared on identical inputs.
+// Register-resident path iff the node-major padded system fits MAX_NT tiles --
+// a function of dims alone.  dims->force_large (tests) routes a problem through
+// the large-system path so both paths can be compared on identical inputs.
 // Mixed-row problems, extra variables and equality constraints
 // always take the large-system path (it carries the bordered KKT step).
 bool is_big(const mhe_dims* dm) {
-  const char* f = getenv("MHE_FORCE_BIG");
-  if (f && f[0] == '1') return true;
+  if (dm->force_large) return true;
   if (dm->meas_model == MHE_MEAS_MIXED || dm->n_extra > 0 || dm->n_eq > 0) return true;
   return ((dm->N + 1) * dm->n + 15) / 16 > MAX_NT;
 }
@@ -1506,24 +1701,46 @@ int check_dims(const mhe_dims* dm, int* NT_out) {
   return MHE_OK;
 }
 
-int smem_bytes(const mhe_dims* dm, int NT) {
+int smem_bytes(const mhe_dims* dm, int NT, bool bounded = false) {
   int p, q;
   bool lin;
   meas_info(dm->meas_model, dm->n, p, q, lin);
-  return smem_layout(dm->N + 1, dm->M, dm->n, NT, !lin).total * (int)sizeof(double);
+  return smem_layout(dm->N + 1, dm->M, dm->n, NT, !lin, bounded).total * (int)sizeof(double);
 }
+
+// bytes of the constants proper (the stamp follows, in its own 256-B block)
+size_t const_payload_bytes(const mhe_dims* dm, int NT) {
+  if (is_big(dm)) return big_const_layout(dm->N + 1, dm->M, dm->n, dm->p, dm->n_eq).total;
+  return const_layout(dm->N + 1, dm->M, dm->n, dm->p, NT).total;
+}
+
+// FNV-1a over the dims that define the constants' layout and contents
+unsigned long long const_tag(const mhe_dims* dm, int NT) {
+  unsigned long long h = 1469598103934665603ull;
+  const long long v[] = {0x4D4845, is_big(dm) ? 1 : 0, dm->N, dm->n, dm->m, dm->p, dm->M, dm->q, dm->dyn_model,
+                         dm->meas_model, dm->has_prior, dm->dyn_cost, NT, dm->n_eq, dm->n_extra};
+  for (long long x : v) {
+    h ^= (unsigned long long)x;
+    h *= 1099511628211ull;
+  }
+  return h | 1ull;
+}
+
+__global__ void k_write_tag(unsigned long long* p, unsigned long long tag) { *p = tag; }
 
 template <class DYN, class MEAS>
 int launch_gn(const mhe_dims* dm, GnArgs& a, int batch, int mode, hipStream_t st) {
   if constexpr (MEAS::MIXED) {
     return MHE_ERR_UNSUPPORTED;  // mixed rows: large-system path only
   } else {
-  int smem = smem_bytes(dm, a.NT);
+  const bool bounded = mode == MODE_SOLVE && dm->n_bounds > 0;
+  int smem = smem_bytes(dm, a.NT, bounded);
   if (const char* pad = getenv("MHE_DEBUG_SMEM_PAD")) smem += atoi(pad);  // debug: force occupancy
   if (smem > 160 * 1024) return MHE_ERR_UNSUPPORTED;
   void (*kern)(GnArgs) = nullptr;
   const bool huber = dm->dyn_cost == MHE_COST_HUBER;
-  if (mode == MODE_SOLVE) kern = huber ? k_gn<DYN, MEAS, MAX_SLOTS, MODE_SOLVE, true> : k_gn<DYN, MEAS, MAX_SLOTS, MODE_SOLVE>;
+  if (bounded) kern = huber ? k_gn_bounded<DYN, MEAS, MAX_SLOTS, true> : k_gn_bounded<DYN, MEAS, MAX_SLOTS>;
+  else if (mode == MODE_SOLVE) kern = huber ? k_gn<DYN, MEAS, MAX_SLOTS, MODE_SOLVE, true> : k_gn<DYN, MEAS, MAX_SLOTS, MODE_SOLVE>;
   else if (mode == MODE_ASSEMBLE)
     kern = huber ? k_gn<DYN, MEAS, MAX_SLOTS, MODE_ASSEMBLE, true> : k_gn<DYN, MEAS, MAX_SLOTS, MODE_ASSEMBLE>;
   else kern = k_gn<DYN, MEAS, MAX_SLOTS, MODE_LINSOLVE>;
@@ -1625,6 +1842,8 @@ GnArgs make_args(const mhe_dims* dm, const void* cbuf, int NT) {
   a.alpha = 2.0 / dm->T;
   a.huber_delta = dm->huber_delta;
   a.n_bounds = dm->n_bounds;
+  a.tag_off = const_payload_bytes(dm, NT);
+  a.tag = const_tag(dm, NT);
   for (int i = 0; i < 8; ++i) {
     a.bidx[i] = dm->bound_idx[i];
     a.blb[i] = dm->bound_lb[i];
@@ -1677,14 +1896,27 @@ struct LaunchBig {
     if (K > 0 && hipFuncSetAttribute((const void*)k_big_border<DYN::n, MEAS::p>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      smem_b) != hipSuccess)
       return MHE_ERR_HIP;
-    hipLaunchKernelGGL(k_big_init, dim3((batch + 255) / 256), dim3(256), 0, st, batch, A.state, A.iters);
+    hipLaunchKernelGGL(k_big_init, dim3((batch + 255) / 256), dim3(256), 0, st, A, batch);
+    const bool bounded = A.n_bounds > 0;
+    const int smem_ls = A.P * A.n * (int)sizeof(double);
+    if (bounded) {
+      if (smem_ls > 128 * 1024) return MHE_ERR_UNSUPPORTED;
+      if (hipFuncSetAttribute((const void*)k_big_linesearch<DYN, MEAS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              smem_ls) != hipSuccess)
+        return MHE_ERR_HIP;
+      const size_t nx = (size_t)batch * A.P * A.n;
+      hipLaunchKernelGGL(k_big_project<DYN::n>, dim3((unsigned)((nx + 255) / 256)), dim3(256), 0, st, A, batch);
+    }
     for (int it = 0; it < max_iter; ++it) {
       hipLaunchKernelGGL((k_big_resid<DYN, MEAS>), dim3(batch), dim3(BIG_NTHREADS), 0, st, A, 0);
       hipLaunchKernelGGL((k_big_assemble<DYN, MEAS>), dim3((npos * BigPairs<DYN::n>::NCH + 3) / 4, batch), dim3(256), 0,
                          st, A);
       hipLaunchKernelGGL(k_big_chol, dim3(batch), dim3(BIG_NTHREADS), smem, st, A);
       if (K > 0) hipLaunchKernelGGL((k_big_border<DYN::n, MEAS::p>), dim3(batch), dim3(BIG_NTHREADS), smem_b, st, A);
-      hipLaunchKernelGGL((k_big_update<DYN::n>), dim3(batch), dim3(256), 0, st, A);
+      if (bounded)
+        hipLaunchKernelGGL((k_big_linesearch<DYN, MEAS>), dim3(batch), dim3(BIG_NTHREADS), smem_ls, st, A);
+      else
+        hipLaunchKernelGGL((k_big_update<DYN::n>), dim3(batch), dim3(256), 0, st, A);
     }
     hipLaunchKernelGGL((k_big_resid<DYN, MEAS>), dim3(batch), dim3(BIG_NTHREADS), 0, st, A, 1);
     hipLaunchKernelGGL(k_big_finish, dim3((batch + 255) / 256), dim3(256), 0, st, batch, A.state);
@@ -1722,8 +1954,7 @@ size_t mhe_workspace_bytes(const mhe_dims* dims, int32_t batch) {
 size_t mhe_const_bytes(const mhe_dims* dims) {
   int NT = 0;
   if (check_dims(dims, &NT) != MHE_OK) return 0;
-  if (is_big(dims)) return big_const_layout(dims->N + 1, dims->M, dims->n, dims->p, dims->n_eq).total;
-  return const_layout(dims->N + 1, dims->M, dims->n, dims->p, NT).total;
+  return const_payload_bytes(dims, NT) + 256;  // + layout stamp
 }
 
 int mhe_build_constants(const mhe_dims* dims, const double* D, const double* cw, const double* Phi,
@@ -1735,7 +1966,11 @@ int mhe_build_constants(const mhe_dims* dims, const double* D, const double* cw,
     return MHE_ERR_NULL;
   hipStream_t st = (hipStream_t)stream;
   BuildCC f{dims, NT, D, cw, Phi, Qw, Rw, Pw, (char*)const_buf, st};
-  return dispatch(dims, f);
+  rc = dispatch(dims, f);
+  if (rc != MHE_OK) return rc;
+  hipLaunchKernelGGL(k_write_tag, dim3(1), dim3(1), 0, st,
+                     (unsigned long long*)((char*)const_buf + const_payload_bytes(dims, NT)), const_tag(dims, NT));
+  return hipGetLastError() == hipSuccess ? MHE_OK : MHE_ERR_HIP;
 }
 
 int mhe_gn_solve(const mhe_dims* dims, const void* const_buf, int32_t batch, const double* X0, double* X_out,
@@ -1789,6 +2024,8 @@ int mhe_gn_solve_ext(const mhe_dims* dims, const void* const_buf, int32_t batch,
     A.nz = dims->n_extra;
     A.nc = dims->n_eq;
     A.Z = Z_out;
+    A.tag_off = const_payload_bytes(dims, NT);
+    A.tag = const_tag(dims, NT);
     LaunchBig f{dims, &A, batch, max_iter, X0, Z0, (hipStream_t)stream};
     return dispatch(dims, f);
   }

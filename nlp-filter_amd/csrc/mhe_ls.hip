@@ -132,8 +132,10 @@ __global__ __launch_bounds__(256) void k_ls(LsArgs a) {
         row_geom(S[3 * q], S[3 * q + 1], S[3 * q + 2], x0, x1, x2, g, nrm);
         accum(A, v, g, RR[q] - (V[3 * q] * -g[0] + V[3 * q + 1] * -g[1] + V[3 * q + 2] * -g[2]));
       }
+      // a singular velocity system leaves v / bd NaN; iters keeps the position fix's
+      // count (velocity failure is told apart from position failure by the NaN)
       double sv[4] = {NAN, NAN, NAN, NAN};
-      if (ns < 4 || !solve4(A, v, sv)) a.iters[e] = -1;
+      if (ns >= 4) (void)solve4(A, v, sv);  // sv untouched (NaN) when singular
       a.v_out[e * 3] = sv[0]; a.v_out[e * 3 + 1] = sv[1]; a.v_out[e * 3 + 2] = sv[2];
       a.bd_out[e] = sv[3];
     }

@@ -13,7 +13,7 @@ LIB_PATH = os.environ.get("MHE_LIB", os.path.join(HERE, "libmhe.so"))
 
 MHE_OK = 0
 ERRORS = {-1: "MHE_ERR_DIMS", -2: "MHE_ERR_MODEL", -3: "MHE_ERR_HIP", -4: "MHE_ERR_UNSUPPORTED", -5: "MHE_ERR_NULL"}
-STATUS = {0: "converged", 1: "max_iter", 2: "not_spd", 3: "nonfinite"}
+STATUS = {0: "converged", 1: "max_iter", 2: "not_spd", 3: "nonfinite", 4: "bad_constants"}
 
 # symbol -> (restype, argtypes); must match include/mhe.h exactly
 c_i32, c_i64, c_dbl, c_vp, c_sz = ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p, ctypes.c_size_t
@@ -27,6 +27,7 @@ class MheDims(ctypes.Structure):
         ("dyn_cost", c_i32), ("n_bounds", c_i32), ("huber_delta", c_dbl),
         ("bound_idx", c_i32 * 8), ("bound_lb", c_dbl * 8), ("bound_ub", c_dbl * 8),
         ("n_extra", c_i32), ("n_eq", c_i32), ("eq_idx", ctypes.POINTER(c_i32)),
+        ("force_large", c_i32),
     ]
 
 
@@ -98,6 +99,14 @@ def load(path=None):
     if path is None:
         _lib = lib
     return lib
+
+
+def lib_digest(path=None):
+    """sha256 (16 hex digits) of the libmhe.so file -- stamps profiles with the
+    exact build they measured (tools/parse_pmc.py, bench.py)."""
+    import hashlib
+    with open(path or LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
 
 
 def check(rc, what):

@@ -4,14 +4,19 @@
 models, measurement times, weights) and solves many independent trajectories
 that share it:  X (B, P, n), U (B|1, P, m), Y (B, M, p), PAR (B|1, M, q),
 x0 (B, n).  Everything is fp64 and stays in HBM between calls; the HIP work is
-enqueued on the current torch stream (or the one passed in).
+enqueued on the current torch stream (or the one passed in: inputs are staged and
+outputs allocated on that stream after it waits for the current one, and every
+tensor the launch touches is kept alive for it -- mhe.streams).  The large-system
+workspace is cached per stream, so concurrent solves on different streams never
+share one.
 """
 import numpy as np
 import torch
 
 from . import _lib, registry
+from .streams import keep_alive, launch_stream
 
-STATUS_CONVERGED, STATUS_MAX_ITER, STATUS_NOT_SPD, STATUS_NONFINITE = 0, 1, 2, 3
+STATUS_CONVERGED, STATUS_MAX_ITER, STATUS_NOT_SPD, STATUS_NONFINITE, STATUS_BAD_CONSTANTS = 0, 1, 2, 3, 4
 
 
 def _dev(x, device, shape=None):
@@ -36,9 +41,8 @@ def ctypes_ptr(t):
     return ctypes.c_void_p(t.data_ptr())
 
 
-def _stream(stream):
+def _handle(s):
     import ctypes
-    s = stream if stream is not None else torch.cuda.current_stream()
     return ctypes.c_void_p(s.cuda_stream)
 
 
@@ -55,15 +59,17 @@ class BatchSolver:
       Pw (n,n)|None   prior information (addInitialCost), None = no prior
       meas_idx        static index parameters of the measurement model
       dyn_cost        "l2" (weighted_l2_norm) or "huber" (pseudo_huber_loss, IRLS; huber_delta)
-      bounds          [(state component, lb, ub), ...] enforced by projected GN (addVarBounds)
+      bounds          [(state component, lb, ub), ...] enforced by projected Newton (addVarBounds)
       n_extra         extra decision variables z (meas="mixed" rows may reference them)
       eq              (K, 2) equality constraints v[a] - v[b] = 0 on the node-major state
                       vector (b = -1: v[a] = 0), met by every GN step (bordered KKT solve)
+      force_large     take the large-system path even when the register-resident kernel
+                      fits (parity tests of the two paths; fixed at construction)
     With meas="mixed", PAR rows follow include/mhe.h (q = 14) and Rw is (M,) weights.
     """
 
     def __init__(self, N, T, dyn, meas, D, cw, Phi, Qw, Rw, Pw=None, meas_idx=None, device="cuda",
-                 dyn_cost="l2", huber_delta=None, bounds=None, n_extra=0, eq=None):
+                 dyn_cost="l2", huber_delta=None, bounds=None, n_extra=0, eq=None, force_large=False):
         self.lib = _lib.load()
         if not torch.cuda.is_available():
             raise _lib.MheLibraryError("no HIP device visible: the estimator has no CPU path")
@@ -109,6 +115,7 @@ class BatchSolver:
             import ctypes
             dims.eq_idx = self._eq.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))  # self._eq keeps it alive
         self.n_eq = dims.n_eq
+        dims.force_large = 1 if force_large else 0
         self.dims = dims
         self.dp = self.lib.mhe_padded_dim(dims)
         if self.dp < 0:
@@ -123,11 +130,14 @@ class BatchSolver:
         self._src = {k: _dev(v, dev) for k, v in self._host.items() if v is not None}
         self.cbuf = torch.empty(nbytes, dtype=torch.uint8, device=dev)
         Pw_t = self._src.get("Pw")
-        self._ws = None
+        self._ws = {}  # large-system workspace per stream handle
+        cur = torch.cuda.current_stream(dev)
         rc = self.lib.mhe_build_constants(
             self.dims, _ptr(self._src["D"]), _ptr(self._src["cw"]), _ptr(self._src["Phi"]),
-            _ptr(self._src["Qw"]), _ptr(self._src["Rw"]), _ptr(Pw_t), _ptr(self.cbuf), _stream(None))
+            _ptr(self._src["Qw"]), _ptr(self._src["Rw"]), _ptr(Pw_t), _ptr(self.cbuf), _handle(cur))
         _lib.check(rc, "mhe_build_constants")
+        self._built = torch.cuda.Event()  # launches on any stream wait for the constants
+        self._built.record(cur)
 
     # ------------------------------------------------------------------ inputs
     def _inputs(self, X, U, Y, PAR, x0):
@@ -166,40 +176,48 @@ class BatchSolver:
         mhe_gn_solve_ws then needs a device workspace (allocated here, cached)."""
         return self.lib.mhe_workspace_bytes(self.dims, 1) > 0
 
-    def _workspace(self, B):
+    def _workspace(self, B, s):
+        """Workspace for B trajectories on stream s (allocated on s: one per stream, so
+        concurrent solves on different streams never share or free each other's)."""
         nb = self.lib.mhe_workspace_bytes(self.dims, B)
         if nb == 0:
             return None, 0
-        if self._ws is None or self._ws.numel() < nb:
-            self._ws = torch.empty(nb, dtype=torch.uint8, device=self.device)
-        return self._ws, nb
+        ws = self._ws.get(s.cuda_stream)
+        if ws is None or ws.numel() < nb:
+            ws = torch.empty(nb, dtype=torch.uint8, device=self.device)
+            self._ws[s.cuda_stream] = ws
+        return ws, nb
 
-    def _gn(self, B, X, Xo, U_t, ustr, Y_t, PAR_t, pstr, x0_t, cost, iters, status, max_iter, tol, stream,
+    def _gn(self, s, cur, B, X, Xo, U_t, ustr, Y_t, PAR_t, pstr, x0_t, cost, iters, status, max_iter, tol,
             Z=None, Zo=None):
-        ws, nb = self._workspace(B)
+        ws, nb = self._workspace(B, s)
         rc = self.lib.mhe_gn_solve_ext(self.dims, _ptr(self.cbuf), B, _ptr(X), _ptr(Xo), _ptr(Z), _ptr(Zo),
                                        _ptr(U_t), ustr, _ptr(Y_t), _ptr(PAR_t), pstr, _ptr(x0_t), _ptr(cost),
                                        _ptr(iters), _ptr(status), int(max_iter), float(tol), _ptr(ws), nb,
-                                       _stream(stream))
+                                       _handle(s))
         _lib.check(rc, "mhe_gn_solve_ext")
+        keep_alive(s, cur, X, Xo, Z, Zo, U_t, Y_t, PAR_t, x0_t, cost, iters, status, ws)
 
     # ------------------------------------------------------------------ calls
     def solve(self, X0, U, Y, PAR=None, x0=None, max_iter=20, tol=1e-10, stream=None, out=None, Z0=None):
         """Gauss-Newton to convergence. Returns (X, cost, iters, status) device tensors,
-        and the extra variables Z (B, n_extra) as a fifth element when n_extra > 0."""
-        X, B, U_t, ustr, Y_t, PAR_t, pstr, x0_t = self._inputs(X0, U, Y, PAR, x0)
-        if out is None:
-            Xo = torch.empty_like(X)
-            cost = torch.empty(B, dtype=torch.float64, device=self.device)
-            iters = torch.empty(B, dtype=torch.int32, device=self.device)
-            status = torch.empty(B, dtype=torch.int32, device=self.device)
-        else:
-            Xo, cost, iters, status = out
-        Z = Zo = None
-        if self.n_extra:
-            Z = _dev(np.zeros((B, self.n_extra)) if Z0 is None else Z0, self.device, (B, self.n_extra))
-            Zo = torch.empty_like(Z)
-        self._gn(B, X, Xo, U_t, ustr, Y_t, PAR_t, pstr, x0_t, cost, iters, status, max_iter, tol, stream, Z, Zo)
+        and the extra variables Z (B, n_extra) as a fifth element when n_extra > 0.
+        With ``stream`` the work (staging included) is ordered on that stream; consume
+        the outputs there or make the consuming stream wait for it."""
+        with launch_stream(stream, self.device, (self._built,)) as (s, cur):
+            X, B, U_t, ustr, Y_t, PAR_t, pstr, x0_t = self._inputs(X0, U, Y, PAR, x0)
+            if out is None:
+                Xo = torch.empty_like(X)
+                cost = torch.empty(B, dtype=torch.float64, device=self.device)
+                iters = torch.empty(B, dtype=torch.int32, device=self.device)
+                status = torch.empty(B, dtype=torch.int32, device=self.device)
+            else:
+                Xo, cost, iters, status = out
+            Z = Zo = None
+            if self.n_extra:
+                Z = _dev(np.zeros((B, self.n_extra)) if Z0 is None else Z0, self.device, (B, self.n_extra))
+                Zo = torch.empty_like(Z)
+            self._gn(s, cur, B, X, Xo, U_t, ustr, Y_t, PAR_t, pstr, x0_t, cost, iters, status, max_iter, tol, Z, Zo)
         if self.n_extra:
             return Xo, cost, iters, status, Zo
         return Xo, cost, iters, status
@@ -211,31 +229,36 @@ class BatchSolver:
     def solve_staged(self, staged, outs, max_iter, tol, stream=None):
         X, B, U_t, ustr, Y_t, PAR_t, pstr, x0_t = staged
         Xo, cost, iters, status = outs
-        self._gn(B, X, Xo, U_t, ustr, Y_t, PAR_t, pstr, x0_t, cost, iters, status, max_iter, tol, stream)
+        with launch_stream(stream, self.device, (self._built,)) as (s, cur):
+            self._gn(s, cur, B, X, Xo, U_t, ustr, Y_t, PAR_t, pstr, x0_t, cost, iters, status, max_iter, tol)
 
     def assemble(self, X, U, Y, PAR=None, x0=None, stream=None):
         """GN normal equations at X: H (B,dp,dp), g (B,dp), cost (B)."""
-        X, B, U_t, ustr, Y_t, PAR_t, pstr, x0_t = self._inputs(X, U, Y, PAR, x0)
-        H = torch.empty((B, self.dp, self.dp), dtype=torch.float64, device=self.device)
-        g = torch.empty((B, self.dp), dtype=torch.float64, device=self.device)
-        cost = torch.empty(B, dtype=torch.float64, device=self.device)
-        rc = self.lib.mhe_assemble(self.dims, _ptr(self.cbuf), B, _ptr(X), _ptr(U_t), ustr, _ptr(Y_t), _ptr(PAR_t),
-                                   pstr, _ptr(x0_t), _ptr(H), _ptr(g), _ptr(cost), _stream(stream))
-        _lib.check(rc, "mhe_assemble")
+        with launch_stream(stream, self.device, (self._built,)) as (s, cur):
+            X, B, U_t, ustr, Y_t, PAR_t, pstr, x0_t = self._inputs(X, U, Y, PAR, x0)
+            H = torch.empty((B, self.dp, self.dp), dtype=torch.float64, device=self.device)
+            g = torch.empty((B, self.dp), dtype=torch.float64, device=self.device)
+            cost = torch.empty(B, dtype=torch.float64, device=self.device)
+            rc = self.lib.mhe_assemble(self.dims, _ptr(self.cbuf), B, _ptr(X), _ptr(U_t), ustr, _ptr(Y_t),
+                                       _ptr(PAR_t), pstr, _ptr(x0_t), _ptr(H), _ptr(g), _ptr(cost), _handle(s))
+            _lib.check(rc, "mhe_assemble")
+            keep_alive(s, cur, X, U_t, Y_t, PAR_t, x0_t, H, g, cost)
         return H, g, cost
 
     def chol_solve(self, H, g, stream=None):
         """delta = -H^{-1} g with the solver's tiled Cholesky (H: (B,dp,dp) SPD)."""
-        H = _dev(H, self.device)
-        g = _dev(g, self.device)
-        B = H.shape[0]
-        if H.shape[1:] != (self.dp, self.dp) or g.shape != (B, self.dp):
-            raise ValueError(f"H must be (B,{self.dp},{self.dp}) and g (B,{self.dp})")
-        delta = torch.empty((B, self.dp), dtype=torch.float64, device=self.device)
-        status = torch.empty(B, dtype=torch.int32, device=self.device)
-        rc = self.lib.mhe_chol_solve(self.dims, _ptr(self.cbuf), B, _ptr(H), _ptr(g), _ptr(delta), _ptr(status),
-                                     _stream(stream))
-        _lib.check(rc, "mhe_chol_solve")
+        with launch_stream(stream, self.device, (self._built,)) as (s, cur):
+            H = _dev(H, self.device)
+            g = _dev(g, self.device)
+            B = H.shape[0]
+            if H.shape[1:] != (self.dp, self.dp) or g.shape != (B, self.dp):
+                raise ValueError(f"H must be (B,{self.dp},{self.dp}) and g (B,{self.dp})")
+            delta = torch.empty((B, self.dp), dtype=torch.float64, device=self.device)
+            status = torch.empty(B, dtype=torch.int32, device=self.device)
+            rc = self.lib.mhe_chol_solve(self.dims, _ptr(self.cbuf), B, _ptr(H), _ptr(g), _ptr(delta),
+                                         _ptr(status), _handle(s))
+            _lib.check(rc, "mhe_chol_solve")
+            keep_alive(s, cur, H, g, delta, status)
         return delta, status
 
 

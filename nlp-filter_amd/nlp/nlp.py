@@ -21,8 +21,9 @@ Kept semantics
     missing name or before ``solve()`` (nlp/nlp.py:85-119)
 
   * ``pseudo_huber_loss`` dynamics cost (cost_functions.py:25-31) -> IRLS on the GPU
-  * ``addVarBounds`` on the state trajectory -> projected Gauss-Newton (steps are
-    clipped to the box); bounds on other variables are checked after the solve
+  * ``addVarBounds`` on the state trajectory -> projected Newton on the GN model
+    (epsilon-active set, reduced step, Armijo search along the projection arc: the
+    solution is a KKT point); bounds on other variables are checked after the solve
     (``self.solver["bounds_violated"]``)
   * several measurement plug-ins in one problem (one ``addResidualCost`` call
     each, gnss-multi-receiver.py:70-140), extra decision variables used inside
@@ -304,7 +305,7 @@ class fixedTimeOptimalEstimationNLP(NLP):
 
     def addVarBounds(self, X, idx, lb, ub):
         """nlp/nlp.py:314-317.  Bounds on a component of the state trajectory are
-        enforced by projected Gauss-Newton (every step is clipped to the box);
+        enforced by the projected Newton method (KKT point of the bounded problem);
         bounds on other variables are recorded and checked after solve()."""
         self._bounds.append((X, idx, lb, ub))
 

@@ -57,11 +57,27 @@ def run_batch(dyn_func, meas_func, mu0, S0, U, Z, nz, Q, R, dt, sat_pos, device=
     (lane when every R block is diagonal -- one device-side check).
 
     inputs="batch_inner": U, Z, nz, sat_pos are given batch-innermost instead,
-    (T,m,B), (T,pmax,B), (T,B), (T,pmax,3,B) -- the device reads then coalesce."""
+    (T,m,B), (T,pmax,B), (T,B), (T,pmax,3,B) -- the device reads then coalesce.
+
+    stream: a torch stream to order the work on (default: the current one); outputs
+    belong to it (mhe.streams)."""
     import torch
+
+    from mhe.streams import launch_stream
 
     (did, n, m), (mid, _, q) = models(dyn_func, meas_func)
     dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    with launch_stream(stream, dev) as (s, cur):
+        return _run_batch(did, n, m, mid, q, dev, s, cur, mu0, S0, U, Z, nz, Q, R, dt, sat_pos, keep_history,
+                          method, inputs)
+
+
+def _run_batch(did, n, m, mid, q, dev, s, cur, mu0, S0, U, Z, nz, Q, R, dt, sat_pos, keep_history, method,
+               inputs):
+    """run_batch on torch stream s (staging and allocation ordered on s)."""
+    import torch
+
+    from mhe.streams import keep_alive
 
     def d(a, dt_=torch.float64):
         return torch.as_tensor(np.asarray(a) if not torch.is_tensor(a) else a, dtype=dt_, device=dev).contiguous()
@@ -109,11 +125,11 @@ def run_batch(dyn_func, meas_func, mu0, S0, U, Z, nz, Q, R, dt, sat_pos, device=
     dims = _lib.MheEkfDims(n=n, m=m, pmax=pmax, q=q, dyn_model=did, meas_model=mid, dt=float(dt),
                            r_diag=int(r_diag), hist_batch_inner=1, in_batch_inner=int(bi))
     lib = _lib.load()
-    sh = stream.cuda_stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
     rc = lib.mhe_ekf_run(ctypes.byref(dims), B, T, _ptr(mu), _ptr(S), _ptr(Ut), T * m, _ptr(Zt), T * pmax,
                          _ptr(nzt), T, _ptr(Pt), T * pmax * q, _ptr(Qt), _ptr(Rt), r_b, r_s, _ptr(mh_st),
-                         _ptr(Sh_st), _ptr(st), ctypes.c_void_p(sh))
+                         _ptr(Sh_st), _ptr(st), ctypes.c_void_p(s.cuda_stream))
     _lib.check(rc, "mhe_ekf_run")
+    keep_alive(s, cur, mu, S, Ut, Zt, nzt, Pt, Qt, Rt, mh_st, Sh_st, st)
     mh = mh_st.permute(2, 0, 1) if keep_history else None
     Sh = Sh_st.permute(3, 0, 1, 2) if keep_history else None
     return mh, Sh, mu, S, st

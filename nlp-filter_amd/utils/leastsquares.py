@@ -7,10 +7,10 @@ Same entry points and semantics as the reference:
       previous fix exactly as the reference's mutable default does;
   ``iterativeLeastSquaresVel(sat_pos, sat_vel, pr_rate, x)``            (:45-63)
   ``runLeastSquares(t, sat_pos, pr, sat_vel, pr_rate, p_ref_ECEF)``     (:97-141)
-      the per-epoch loop, as ONE launch (one wavefront walks the epochs in order,
+      the per-epoch loop, as ONE launch (one lane walks the epochs in order,
       carrying the warm start), same result dict;
-  ``run_batch(...)``: many logs at once (one wavefront per log, or with
-      ``warm=False`` one wavefront per epoch).
+  ``run_batch(...)``: many logs at once (one lane per log, or with
+      ``warm=False`` one lane per epoch).
 Every solve runs in ``mhe_ls_run`` (csrc/mhe_ls.hip); without libmhe.so the
 calls raise ``MheLibraryError``.  ``buildGeometryMatrix`` is the reference's
 host helper (:6-16), kept for API parity.
@@ -19,7 +19,8 @@ Numerics: the reference solves pinv(G) drho; the kernel solves the 4x4 normal
 equations by Cholesky -- the same least-squares solution for a full-rank G,
 equal to rounding (tests state the tolerance).  Epochs with fewer than four
 independent satellites report iters = -1 (the reference's pinv would return a
-minimum-norm step there).
+minimum-norm step there); a singular velocity system leaves v and bd NaN and the
+position fix's iteration count untouched.
 """
 import ctypes
 
@@ -51,11 +52,22 @@ def run_batch(sat_pos, pr, nsat, x_init=None, sat_vel=None, pr_rate=None, warm=T
     x_init (C,3) starting position (default zeros); sat_vel / pr_rate (C,T,S[,3])
     add the velocity solve.  NumPy or torch inputs.  Returns a dict of device
     tensors: x (C,T,3), b (C,T), iters (C,T), x_last (C,3) and, with velocities,
-    v (C,T,3), bd (C,T)."""
+    v (C,T,3), bd (C,T).  stream: a torch stream to order the work on (default:
+    the current one); outputs belong to it (mhe.streams)."""
     import torch
+
+    from mhe.streams import keep_alive, launch_stream
 
     lib = _lib.load()
     dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    with launch_stream(stream, dev) as (s, cur):
+        out, used = _run_batch(lib, dev, s, sat_pos, pr, nsat, x_init, sat_vel, pr_rate, warm, maxiter, tol)
+        keep_alive(s, cur, *used)
+    return out
+
+
+def _run_batch(lib, dev, s, sat_pos, pr, nsat, x_init, sat_vel, pr_rate, warm, maxiter, tol):
+    import torch
 
     def d(a, dt=torch.float64):
         return None if a is None else torch.as_tensor(a, dtype=dt, device=dev).contiguous()
@@ -78,12 +90,11 @@ def run_batch(sat_pos, pr, nsat, x_init=None, sat_vel=None, pr_rate=None, warm=T
         out["bd"] = torch.empty((C, T), dtype=torch.float64, device=dev)
     dims = _lib.MheLsDims(slots=S, max_iter=int(maxiter), warm=1 if warm else 0, with_vel=1 if with_vel else 0,
                           tol=float(tol))
-    st = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
     rc = lib.mhe_ls_run(ctypes.byref(dims), C, T, _ptr(sp), _ptr(prt), _ptr(ns), _ptr(sv), _ptr(rr), _ptr(xi),
                         _ptr(out["x"]), _ptr(out["b"]), _ptr(out.get("v")), _ptr(out.get("bd")),
-                        _ptr(out["iters"]), _ptr(out["x_last"]) if warm else None, ctypes.c_void_p(st))
+                        _ptr(out["iters"]), _ptr(out["x_last"]) if warm else None, ctypes.c_void_p(s.cuda_stream))
     _lib.check(rc, "mhe_ls_run")
-    return out
+    return out, [sp, prt, ns, sv, rr, xi] + list(out.values())
 
 
 def _pack(sat_pos_list, values_lists, S=None):

@@ -13,9 +13,11 @@ Gauss-Newton on J (the same stationary point IPOPT returns for this
 unconstrained problem): H delta = -g with H = sum A^T W A, g = sum A^T W r.
 With the pseudo-Huber dynamics cost (cost_functions.py:25-31) the step is IRLS:
 per defect component W r -> rho'(r)/2 and W -> diag(rho'(r)/(2r)).
-With addVarBounds (nlp/nlp.py:314-317) the step is projected onto the box
-(projected Gauss-Newton; IPOPT's interior point reaches the same point when the
-bounds are inactive).
+With addVarBounds (nlp/nlp.py:314-317) the iteration is a projected Newton method
+on the GN model (epsilon-active set, reduced system on the free entries, Armijo
+search along the projection arc; ``gauss_newton_bounded``): its limit points are
+KKT points of the bound-constrained problem, the point IPOPT's interior-point
+method converges to.
 
 Two independent forms are provided:
   * ``normal_equations``          structured (Kronecker) form, vectorised over the batch
@@ -208,7 +210,11 @@ def gauss_newton(pb, X0, U, Y, PAR=None, x0=None, max_iter=20, tol=1e-10):
     Per trajectory: solve H delta = -g (Cholesky), X += delta, iters += 1;
     converged when max|delta| <= tol * (1 + max|X|). Converged trajectories are
     frozen. Returns X, cost (at the returned X), iters, status.
+    With bounds (pb.lb / pb.ub) the iteration is the projected Newton method of
+    ``gauss_newton_bounded``.
     """
+    if pb.lb is not None or pb.ub is not None:
+        return gauss_newton_bounded(pb, X0, U, Y, PAR, x0, max_iter, tol)
     X = np.array(X0, dtype=np.float64, copy=True)
     B = X.shape[0]
     iters = np.zeros(B, dtype=np.int32)
@@ -236,20 +242,127 @@ def gauss_newton(pb, X0, U, Y, PAR=None, x0=None, max_iter=20, tol=1e-10):
                 active[b] = False
                 continue
             step = delta.reshape(X.shape[1:])
-            xn = X[b] + step
-            if pb.lb is not None or pb.ub is not None:  # projected step (addVarBounds)
-                lo = -np.inf if pb.lb is None else pb.lb
-                hi = np.inf if pb.ub is None else pb.ub
-                xc = np.minimum(np.maximum(xn, lo), hi)
-                step = np.where(xc != xn, xc - X[b], step)
-                xn = xc
-            X[b] = xn
+            X[b] = X[b] + step
             iters[b] += 1
             if np.max(np.abs(step)) <= tol * (1.0 + np.max(np.abs(X[b]))):
                 status[b] = OK
                 active[b] = False
     _, _, _, cost = residuals(pb, X, U, Y, PAR, x0)
     return X, cost, iters, status
+
+
+# Projected Newton (Bertsekas 1982, "Projected Newton methods for optimization
+# problems with simple constraints") on the Gauss-Newton model, for addVarBounds
+# (nlp/nlp.py:314-317: lb <= x[idx] <= ub at every node).  Constants shared with
+# the HIP kernels (k_gn_bounded, k_big_linesearch):
+EPS_ACT = 1e-6       # epsilon-active set: eps = min(EPS_ACT (1 + max|X|), w)
+ARMIJO_SIGMA = 1e-4  # sufficient decrease along the projection arc
+LS_MAX = 30          # step halvings; the last trial is taken if none is accepted
+COST_SLACK = 1e-12   # relative cost slack of the Armijo test: near a solution the decrease
+                     # falls below the cost's rounding error and full steps must pass
+
+
+def box(pb, shape):
+    """(lo, hi) arrays of `shape` (..., n) from the per-component bounds."""
+    lo = np.broadcast_to(-np.inf if pb.lb is None else pb.lb, shape)
+    hi = np.broadcast_to(np.inf if pb.ub is None else pb.ub, shape)
+    return lo, hi
+
+
+def active_set(pb, X, g):
+    """epsilon-active set of the projected Newton method at X with half-gradient g
+    (both (P, n)): bounded entries within eps of a bound whose gradient points out of
+    the box.  w = max |X - P(X - g)| over the bounded entries (0 at a KKT point), so
+    eps -> 0 at a solution and the set becomes the exact binding set."""
+    lo, hi = box(pb, X.shape)
+    bounded = np.isfinite(lo) | np.isfinite(hi)
+    w = np.max(np.abs(X - np.clip(X - g, lo, hi)), where=bounded, initial=0.0)
+    eps = min(EPS_ACT * (1.0 + np.max(np.abs(X))), w)
+    return bounded & (((X <= lo + eps) & (g > 0)) | ((X >= hi - eps) & (g < 0)))
+
+
+def gauss_newton_bounded(pb, X0, U, Y, PAR=None, x0=None, max_iter=20, tol=1e-10):
+    """Gauss-Newton with bounds as a projected Newton method (per trajectory):
+
+      X <- P(X0)                                   (P: projection onto the box)
+      repeat:  H, g at X   (g = J^T W r = half the gradient of the cost)
+        A  = active_set(X, g)
+        Ht = H with the rows / columns of A replaced by their diagonal entries
+        d  = -Ht^-1 g                               (reduced GN step on the free set,
+                                                     diagonally scaled gradient on A)
+        s  = P(X + d) - X                           (stationarity: s = 0 at a KKT point)
+        a = 1, 1/2, ... (LS_MAX trials): X(a) = P(X + a d) until
+          cost(X(a)) <= cost(X) + 2 sigma [sum_free a g.d + sum_A g.(X(a) - X)]
+                         + COST_SLACK |cost(X)|
+        X <- X(a);  converged when max|s| <= tol (1 + max|X|).
+    Limit points are KKT points of the bound-constrained least-squares problem (the
+    fixed point of plain step clipping is not).  Returns X, cost, iters, status."""
+    X = np.array(X0, dtype=np.float64, copy=True)
+    B = X.shape[0]
+    lo, hi = box(pb, X.shape[1:])
+    X = np.clip(X, lo, hi)
+    iters = np.zeros(B, dtype=np.int32)
+    status = np.full(B, MAXITER, dtype=np.int32)
+    cost_out = np.zeros(B)
+
+    def one(A, b):
+        return None if A is None else A[b:b + 1] if A.shape[0] == B else A
+
+    for b in range(B):
+        pbs = _with_rw(pb, pb.Rw[b:b + 1]) if pb.Rw.ndim == 4 else pb
+        args = (one(U, b), Y[b:b + 1], one(PAR, b), one(x0, b))
+        Xb = X[b:b + 1].copy()
+        while True:
+            H, g, J = normal_equations(pbs, Xb, *args)
+            if iters[b] >= max_iter:
+                break
+            H, g, J = H[0], g[0], J[0]
+            act = active_set(pb, Xb[0], g.reshape(Xb.shape[1:])).ravel()
+            dH = np.diag(H).copy()
+            H[act, :] = 0.0
+            H[:, act] = 0.0
+            H[act, act] = dH[act]
+            try:
+                L = np.linalg.cholesky(H)
+            except np.linalg.LinAlgError:
+                status[b] = NOT_SPD
+                break
+            d = -np.linalg.solve(L.T, np.linalg.solve(L, g))
+            if not np.all(np.isfinite(d)):
+                status[b] = NONFINITE
+                break
+            d = d.reshape(Xb.shape[1:])
+            x = Xb[0]
+            s = np.clip(x + d, lo, hi) - x
+            actr = act.reshape(x.shape)
+            gr = g.reshape(x.shape)
+            alpha = 1.0
+            for _ in range(LS_MAX):
+                xt = np.clip(x + alpha * d, lo, hi)
+                pred = alpha * np.sum(np.where(actr, 0.0, gr * d)) + np.sum(np.where(actr, gr * (xt - x), 0.0))
+                Jt = residuals(pbs, xt[None], *args)[3][0]
+                if Jt <= J + 2.0 * ARMIJO_SIGMA * pred + COST_SLACK * abs(J):
+                    break
+                alpha *= 0.5
+            Xb = xt[None]
+            iters[b] += 1
+            if np.max(np.abs(s)) <= tol * (1.0 + np.max(np.abs(xt))):
+                status[b] = OK
+                H, g, J = normal_equations(pbs, Xb, *args)
+                break
+        X[b] = Xb[0]
+        cost_out[b] = np.asarray(J).reshape(-1)[0]
+    return X, cost_out, iters, status
+
+
+def kkt_residual(pb, X, U, Y, PAR=None, x0=None):
+    """Bound-constrained stationarity at X (B, P, n): max over entries of
+    |X - P(X - grad)| with grad = 2 g the cost gradient -- zero exactly at KKT points
+    (free entries: grad = 0; at a lower bound grad >= 0; at an upper bound grad <= 0)."""
+    _, g, _ = normal_equations(pb, X, U, Y, PAR, x0)
+    lo, hi = box(pb, X.shape)
+    grad = 2.0 * g.reshape(X.shape)
+    return np.max(np.abs(X - np.clip(X - grad, lo, hi)).reshape(X.shape[0], -1), axis=1)
 
 
 def gn_step_batched(pb, X, U, Y, PAR=None, x0=None):

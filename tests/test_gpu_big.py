@@ -4,10 +4,9 @@ register-resident kernel and the CPU oracle.
 Tolerances as tests/test_gpu_parity.py: iterates <= 1e-9 kappa (1 + max|X|) after
 the same number of iterations, converged optimum <= 1e-8 kappa (1 + max|X|),
 kappa = max|y| / max|y - h(x)| (pseudorange cancellation); iteration counts and
-statuses exact.  MHE_FORCE_BIG=1 (debug knob) routes C2 through the large-system
+statuses exact.  force_large=True (mhe_dims.force_large) routes C2 through the large-system
 path, so the two device paths are compared on identical inputs.
 """
-import os
 
 import numpy as np
 import pytest
@@ -43,23 +42,32 @@ def _np(ts):
 
 
 def _forced_big(w):
-    os.environ["MHE_FORCE_BIG"] = "1"
-    try:
-        s = solver.from_workload(w)
-        assert s.large_system
-        return s
-    finally:
-        os.environ.pop("MHE_FORCE_BIG", None)
+    s = solver.from_workload(w, force_large=True)
+    assert s.large_system
+    return s
 
 
 def _solve_forced(s, w, **kw):
-    os.environ["MHE_FORCE_BIG"] = "1"
-    try:
-        out = _np(s.solve(w.X_init, w.U, w.Y, w.PAR, **kw))
-        torch.cuda.synchronize()
-        return out
-    finally:
-        os.environ.pop("MHE_FORCE_BIG", None)
+    out = _np(s.solve(w.X_init, w.U, w.Y, w.PAR, **kw))
+    torch.cuda.synchronize()
+    return out
+
+
+def test_constants_of_other_dims_are_refused_on_device():
+    """the path and layout are fixed when the constants are built; a
+    solve with dims that disagree (here: the other path) computes nothing and says so."""
+    w = configs.make_c2(B=2, N=20)
+    reg = solver.from_workload(w)
+    big = solver.from_workload(w, force_large=True)
+    assert not reg.large_system and big.large_system
+    for s, other in ((reg, big), (big, reg)):
+        s.cbuf, saved = other.cbuf, s.cbuf   # constants laid out for the other path
+        try:
+            X, cost, iters, status = _np(s.solve(w.X_init, w.U, w.Y, max_iter=3))
+        finally:
+            s.cbuf = saved
+        assert status.tolist() == [solver.STATUS_BAD_CONSTANTS] * 2 and iters.tolist() == [0, 0]
+        assert np.array_equal(X, w.X_init) and np.isnan(cost).all()
 
 
 def test_forced_big_path_matches_register_path_c2():

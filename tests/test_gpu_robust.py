@@ -1,12 +1,11 @@
-"""Pseudo-Huber dynamics cost (IRLS) and variable bounds (projected GN) on the GPU
-vs the CPU oracle (oracle/gn.py: same iteration -- cost_functions.py:25-31,
-nlp/nlp.py:314-317).
+"""Pseudo-Huber dynamics cost (IRLS) and variable bounds (projected Newton with an
+Armijo search along the projection arc) on the GPU vs the CPU oracle (oracle/gn.py:
+same iteration -- cost_functions.py:25-31, nlp/nlp.py:314-317).
 
 Tolerances as tests/test_gpu_parity.py: assembled H, g <= 1e-12 relative; iterates
 <= 1e-9 (1 + max|X|) after the same number of iterations; converged <= 1e-8;
 bound satisfaction exact (the projection clips to the bound value).
 """
-import os
 
 import numpy as np
 import pytest
@@ -70,27 +69,47 @@ def _check_bounds(w, X, cost, iters, status, pb):
     Xr, cr, ir, sr = gn.gauss_newton(pb, w.X_init, _U(w), w.Y, max_iter=30, tol=1e-10)
     assert (X[:, :, 1] >= 0.5).all() and (X[:, :, 0] <= 1.5).all()
     assert (X[:, :, 1] == 0.5).any(), "the test bound should be active"
-    assert status.tolist() == sr.tolist() and np.all(np.abs(iters - ir) <= 1)
+    assert status.tolist() == sr.tolist() == [gn.OK] * w.B and np.all(np.abs(iters - ir) <= 1)
     assert np.abs(X - Xr).max() <= 1e-8 * (1 + np.abs(Xr).max())
     assert np.allclose(cost, cr, rtol=1e-8)
+    # a KKT point of the bound-constrained problem, not just the oracle's iterate
+    lo, hi = gn.box(pb, X.shape)
+    _, g0, _ = gn.normal_equations(pb, np.clip(w.X_init, lo, hi), _U(w), w.Y)
+    assert np.all(gn.kkt_residual(pb, X, _U(w), w.Y) <= 1e-9 * np.abs(2 * g0).max(axis=1))
 
 
-def test_bounds_projected_gn_register_path():
+def test_bounds_iterates_match_oracle_fixed_count():
+    """Same active sets and line-search decisions: iterates after 6 steps (tol 0)."""
+    w, bounds, pb = _bounds_case()
+    s = solver.from_workload(w, bounds=bounds)
+    X, cost, iters, status = _np(s.solve(w.X_init, w.U, w.Y, max_iter=6, tol=0.0))
+    Xr, cr, ir, sr = gn.gauss_newton(pb, w.X_init, _U(w), w.Y, max_iter=6, tol=0.0)
+    assert iters.tolist() == ir.tolist() == [6] * w.B and status.tolist() == sr.tolist()
+    assert np.abs(X - Xr).max() <= 1e-9 * (1 + np.abs(Xr).max())
+    assert np.allclose(cost, cr, rtol=1e-10)
+
+
+def test_bounds_projected_newton_register_path():
     w, bounds, pb = _bounds_case()
     s = solver.from_workload(w, bounds=bounds)
     _check_bounds(w, *_np(s.solve(w.X_init, w.U, w.Y, max_iter=30, tol=1e-10)), pb)
 
 
-def test_bounds_projected_gn_large_system_path():
+def test_bounds_projected_newton_large_system_path():
     w, bounds, pb = _bounds_case()
-    os.environ["MHE_FORCE_BIG"] = "1"
-    try:
-        s = solver.from_workload(w, bounds=bounds)
-        assert s.large_system
-        out = _np(s.solve(w.X_init, w.U, w.Y, max_iter=30, tol=1e-10))
-    finally:
-        os.environ.pop("MHE_FORCE_BIG", None)
-    _check_bounds(w, *out, pb)
+    s = solver.from_workload(w, bounds=bounds, force_large=True)
+    assert s.large_system
+    _check_bounds(w, *_np(s.solve(w.X_init, w.U, w.Y, max_iter=30, tol=1e-10)), pb)
+
+
+def test_bounds_iterates_match_oracle_fixed_count_large_system_path():
+    w, bounds, pb = _bounds_case()
+    s = solver.from_workload(w, bounds=bounds, force_large=True)
+    X, cost, iters, status = _np(s.solve(w.X_init, w.U, w.Y, max_iter=6, tol=0.0))
+    Xr, cr, ir, sr = gn.gauss_newton(pb, w.X_init, _U(w), w.Y, max_iter=6, tol=0.0)
+    assert iters.tolist() == ir.tolist() == [6] * w.B and status.tolist() == sr.tolist()
+    assert np.abs(X - Xr).max() <= 1e-9 * (1 + np.abs(Xr).max())
+    assert np.allclose(cost, cr, rtol=1e-10)
 
 
 def test_huber_on_large_system_path_is_refused():
@@ -116,7 +135,7 @@ def test_facade_huber_and_bounds_match_oracle():
     problem.addResidualCost(measurements.full_state, X, w.t_meas, w.Y[0].T, w.Rw[0])
     problem.addVarBounds(X, 1, 0.5, np.inf)
     problem.initializeEstimate(X, t_nodes, w.X_init[0].T)
-    problem.max_iter, problem.tol = 40, 0.0  # same iteration count on both sides (projected IRLS)
+    problem.max_iter, problem.tol = 40, 0.0  # same iteration count on both sides (projected Newton, IRLS)
     problem.solve()
     Xg = np.stack([problem.extractVariableValue("x", k) for k in range(w.N + 1)])
     pb = _pb(w, dyn_cost="huber", delta=DELTA, lb=[-np.inf, 0.5], ub=[np.inf, np.inf])

@@ -165,3 +165,18 @@ def test_underdetermined_epoch_flagged(lsfx):
     r = uls.run_batch(sp, pr, cnt, warm=False)
     it = r["iters"].cpu().numpy()[0]
     assert it[0] == -1 and it[2] == -1 and it[1] > 0
+
+
+@pytest.mark.gpu
+def test_velocity_failure_reported_by_nan(lsfx):
+    """a velocity solve that cannot be formed leaves v / bd NaN and does
+    not overwrite the position fix's iteration count."""
+    import utils.leastsquares as uls
+    sp = lsfx["A_sat_pos"][None, :2]
+    pr = lsfx["A_pr"][None, :2]
+    cnt = np.array([[3, lsfx["A_count"][1]]], dtype=np.int32)
+    r = uls.run_batch(sp, pr, cnt, warm=False, sat_vel=np.zeros(sp.shape), pr_rate=np.zeros(pr.shape))
+    it = r["iters"].cpu().numpy()[0]
+    v = r["v"].cpu().numpy()[0]
+    assert it[0] == -1 and np.isnan(v[0]).all() and np.isnan(r["bd"].cpu().numpy()[0, 0])
+    assert it[1] > 0 and np.isfinite(v[1]).all()

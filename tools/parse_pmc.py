@@ -4,7 +4,8 @@ HBM traffic per launch = 2 * FETCH_SIZE + WRITE_SIZE (KB -> bytes):
 MI355X_MICROARCH.md §HBM: FETCH_SIZE/WRITE_SIZE are L2 memory-side request
 counters in KB; on gfx950 FETCH_SIZE reports 1/2 of a wide coalesced stream,
 so it is doubled (other access widths are uncalibrated -- stated in the note).
-Writes profiles/pmc_summary.json (read by bench.py for roofline.traffic) and
+Writes profiles/pmc_summary.json (read by bench.py for roofline.traffic, stamped
+with the sha256 of the libmhe.so that was profiled) and
 copies the per-kernel stats CSV to profiles/<tag>_kernel_stats.csv."""
 import csv
 import glob
@@ -14,6 +15,9 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "nlp-filter_amd"))
+from mhe._lib import lib_digest  # noqa: E402
+
 tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
 out = os.path.join(ROOT, "gpurun_out")
 
@@ -49,6 +53,8 @@ busy = mean(per_dispatch("sq", "SQ_VALU_MFMA_BUSY_CYCLES"))
 gui = mean(per_dispatch("sq", "GRBM_GUI_ACTIVE", how="max"))
 summary = {
     "tag": tag, "kernel_sig": "k_gn<DynVanDerPol", "batch": 1024, "iters": 10,
+    # the build these counters measured: bench.py attaches them only to a run of the same libmhe.so
+    "lib_sha": lib_digest(),
     "fetch_size_kb": fetch, "write_size_kb": write,
     "hbm_bytes_per_launch": None if fetch is None or write is None else (2.0 * fetch + write) * 1024.0,
     "mfma_f64_flops_per_launch": None if mops is None else mops * 512.0,
