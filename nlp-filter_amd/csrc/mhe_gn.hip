@@ -62,9 +62,9 @@ __host__ __device__ inline ConstLayout const_layout(int P, int M, int n, int p, 
   L.Cc = o;   o = align256(o + sizeof(double) * ntiles * 256);  // constant part of J^T W J
   L.DA = o;   o = align256(o + sizeof(double) * ntiles * 256);  // a * D[l][j] per tile element
   L.DB = o;   o = align256(o + sizeof(double) * ntiles * 256);  // a * D[j][l] per tile element
-  // n = 2 only: the 8 x 8 node block of D behind each tile, [cn][rn] = a D[8I+cn][8J+rn]
-  // (DAc) and a D[8J+rn][8I+cn] (DBc) -- 512 B per tile instead of 2 KB, spread over
-  // the tile's C layout with ds_bpermute in build_tiles
+  // n = 2 only: the 8 x 8 node block of D behind each tile, a D[8I+cn][8J+rn] (DAc)
+  // and a D[8J+rn][8I+cn] (DBc) -- 512 B per tile instead of 2 KB, one value per lane
+  // in the layout that spread_dblock turns into the tile's C layout (VALU swaps)
   L.DAc = o;  o = align256(o + sizeof(double) * ntiles * 64);
   L.DBc = o;  o = align256(o + sizeof(double) * ntiles * 64);
   L.total = o;
@@ -168,14 +168,6 @@ __device__ __forceinline__ double readlane_d(double v, int lane) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
-// v of lane (byte_addr / 4), per lane (ds_bpermute: LDS crossbar, no LDS storage)
-__device__ __forceinline__ double bpermute_d(int byte_addr, double v) {
-  const long long b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_ds_bpermute(byte_addr, (int)b);
-  const int hi = __builtin_amdgcn_ds_bpermute(byte_addr, (int)(b >> 32));
-  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
-
 // Raw buffer loads from the constants buffer: one resource (SGPRs) over all of
 // cbuf, a per-lane byte offset and a wave-uniform SGPR offset per unrolled term,
 // so each table element costs one buffer_load and no 64-bit address VALU.
@@ -197,6 +189,25 @@ __device__ __forceinline__ double dpp_d(double v) {
   const int lo = __builtin_amdgcn_mov_dpp((int)b, CTRL, 0xF, 0xF, false);
   const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, false);
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// The four alpha D values of a tile element's node pair for registers r = 0..3
+// (n = 2 compact 8 x 8 node blocks, k_build_cc): lane l's value for register r
+// is held by lane (l & ~0x11) | (r & 1) | (r >> 1) << 4, so two DPP quad
+// broadcasts and two v_permlane16_swap pairs spread it -- VALU only, no LDS.
+__device__ __forceinline__ void spread_dblock(double v, double (&o)[4]) {
+  const double ev = dpp_d<0xA0>(v);  // quad_perm [0,0,2,2]: the even lane of each pair
+  const double od = dpp_d<0xF5>(v);  // quad_perm [1,1,3,3]: the odd lane
+  const long long be = __double_as_longlong(ev), bo = __double_as_longlong(od);
+  const auto el = __builtin_amdgcn_permlane16_swap((int)be, (int)be, false, false);
+  const auto eh = __builtin_amdgcn_permlane16_swap((int)(be >> 32), (int)(be >> 32), false, false);
+  const auto ol = __builtin_amdgcn_permlane16_swap((int)bo, (int)bo, false, false);
+  const auto oh = __builtin_amdgcn_permlane16_swap((int)(bo >> 32), (int)(bo >> 32), false, false);
+  // [0]: the even 16-lane row of the pair, [1]: the odd one
+  o[0] = __longlong_as_double(((long long)eh[0] << 32) | (unsigned int)el[0]);
+  o[2] = __longlong_as_double(((long long)eh[1] << 32) | (unsigned int)el[1]);
+  o[1] = __longlong_as_double(((long long)oh[0] << 32) | (unsigned int)ol[0]);
+  o[3] = __longlong_as_double(((long long)oh[1] << 32) | (unsigned int)ol[1]);
 }
 
 // v_permlane16_swap (XOR16 = 1: row pairs) / v_permlane32_swap (2: wave halves)
@@ -706,6 +717,55 @@ __device__ __forceinline__ double h_element(const GnArgs& a, const double* Phi, 
   return v;
 }
 
+// Off-diagonal slots for n = 2 with the L2 dynamics cost and linear measurements
+// (C2's shape), software-pipelined: the six constant loads of slot s + 1 (Cc's
+// four registers, the two compact alpha D blocks; raw buffer loads, one SGPR
+// resource) are issued before slot s is formed, so the slots cost one L2 round
+// trip in all instead of one per load.  Branch-free: an empty slot forms tile 0
+// (never read); padding rows / columns keep -Cc by a select; with n | 16 no
+// off-diagonal tile meets a node's own 2 x 2 block, so F^T E drops out.
+template <int SLOTS, bool BOUNDED>
+__device__ __forceinline__ void build_slots_n2(const GnArgs& a, const ConstLayout& CL, const SmemLayout& SL,
+                                               double* sm, d4 (&acc)[SLOTS], int lane, int stab) {
+  const __amdgpu_buffer_rsrc_t rs = cbuf_rsrc(a.cbuf, CL.total);
+  const double* Es = sm + SL.Es;
+  const int* ACT = (const int*)(sm + SL.ACT);
+  double cn[4], an, bn;
+  auto issue = [&](int s) {
+    const int IJ = slot_ij(stab, s);
+    const int ti = IJ < 0 ? 0 : tile_index(IJ & 0xffff, IJ >> 16, a.NT);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) cn[r] = bload(rs, ti * 2048 + lane * 8, (int)CL.Cc + 512 * r);
+    an = bload(rs, ti * 512 + lane * 8, (int)CL.DAc);
+    bn = bload(rs, ti * 512 + lane * 8, (int)CL.DBc);
+  };
+  issue(0);
+#pragma unroll
+  for (int s = 0; s < SLOTS; ++s) {
+    const double c[4] = {cn[0], cn[1], cn[2], cn[3]};
+    const double av = an, bv = bn;
+    if (s + 1 < SLOTS) issue(s + 1);
+    const int IJ = slot_ij(stab, s);
+    const int I = IJ < 0 ? 1 : IJ & 0xffff, J = IJ < 0 ? 0 : IJ >> 16;
+    const int col = 16 * I + (lane & 15);
+    const int cc = col < a.d ? col : a.d - 1;
+    const int l = cc >> 1, bb = cc & 1;
+    double dav[4], dbv[4];
+    spread_dblock(av, dav);
+    spread_dblock(bv, dbv);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 16 * J + (lane >> 4) + 4 * r;
+      const int rr = row < a.d ? row : a.d - 1;
+      const int j = rr >> 1, aa = rr & 1;
+      const double t = dav[r] * Es[(l * 2 + aa) * 2 + bb] + dbv[r] * Es[(j * 2 + bb) * 2 + aa];
+      acc[s][r] = (row < a.d && col < a.d) ? t - c[r] : -c[r];
+      if (BOUNDED && (ACT[row] | ACT[col])) acc[s][r] = 0.0;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 // Build the H tiles owned by this wave, NEGATED (the factorization accumulates
 // +U^T U into -A, so no operand needs a sign flip).  Slot (I, J), I > J, holds
 // the UPPER block H[J-block][I-block] in the MFMA C layout (lane l, register r: row
@@ -736,8 +796,16 @@ __device__ __forceinline__ void build_tiles(const GnArgs& a, const ConstLayout& 
   asm volatile("" : "+v"(lane));
   asm volatile("" : "+s"(wave));
   asm volatile("" : "+v"(stab));
+  constexpr int n = DYN::n;
+  // Off-diagonal tiles of the common case (L2 dynamics cost, linear measurements):
+  // branch-free.  Padding rows / columns read clamped indices and keep Cc by a
+  // select; when n divides 16 no off-diagonal tile meets a node's diagonal block,
+  // so the F^T E term drops out.  (A per-element branch here costs an exec-mask
+  // round trip and a wait on each LDS read.)
+  constexpr bool FAST = !HUBER && MEAS::LINEAR;
+  if constexpr (FAST && n == 2) build_slots_n2<SLOTS, BOUNDED>(a, CL, SL, sm, acc, lane, stab);
 #pragma unroll
-  for (int s = 0; s < SLOTS; ++s) {
+  for (int s = 0; s < (FAST && n == 2 ? 0 : SLOTS); ++s) {
     const int IJ = slot_ij(stab, s);
     if (IJ < 0) {
       // no tile: always define (keeps acc dead between iterations), but with an
@@ -751,18 +819,45 @@ __device__ __forceinline__ void build_tiles(const GnArgs& a, const ConstLayout& 
       const int ti = tile_index(I, J, a.NT);
       const size_t off = (size_t)ti * 256 + lane;
       const int col = 16 * I + (lane & 15);
-      if constexpr (DYN::n == 2) {
-        // a D_lj / a D_jl of element (row, col) = node pair (8I + cn, 8J + rn) of the
-        // tile's 8 x 8 D block, cn = (lane & 15) >> 1, rn = (lane >> 5) + 2r:
-        // one 512-B load per table, then a lane permute per register
-        const double dac = ((const double*)(a.cbuf + CL.DAc))[(size_t)ti * 64 + lane];
-        const double dbc = ((const double*)(a.cbuf + CL.DBc))[(size_t)ti * 64 + lane];
+      if constexpr (FAST) {
+        const int cc = col < a.d ? col : a.d - 1;
+        const int l = cc / n, bb = cc - l * n;
+        double dav[4], dbv[4];
+        if constexpr (n == 2) {
+          spread_dblock(((const double*)(a.cbuf + CL.DAc))[(size_t)ti * 64 + lane], dav);
+          spread_dblock(((const double*)(a.cbuf + CL.DBc))[(size_t)ti * 64 + lane], dbv);
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int row = 16 * J + (lane >> 4) + 4 * r;
-          const int src = (((lane & 15) >> 1) * 8 + (lane >> 5) + 2 * r) * 4;
-          acc[s][r] = -h_element<DYN, MEAS, HUBER>(a, Phi, Es, FtE, G, Cc[off + 64 * r], bpermute_d(src, dac),
-                                                   bpermute_d(src, dbc), row, col, Dm, LAM);
+          const int rr = row < a.d ? row : a.d - 1;
+          const int j = rr / n, aa = rr - j * n;
+          double da, db;
+          if constexpr (n == 2) {
+            da = dav[r];
+            db = dbv[r];
+          } else {
+            da = DA[off + 64 * r];
+            db = DB[off + 64 * r];
+          }
+          double t = da * Es[(l * n + aa) * n + bb] + db * Es[(j * n + bb) * n + aa];
+          if constexpr (16 % n != 0) t -= j == l ? FtE[(j * n + aa) * n + bb] : 0.0;
+          const double v = Cc[off + 64 * r];
+          acc[s][r] = (row < a.d && col < a.d) ? t - v : -v;
+          if (BOUNDED && (ACT[row] | ACT[col])) acc[s][r] = 0.0;
+        }
+      } else if constexpr (DYN::n == 2) {
+        // a D_lj / a D_jl of element (row, col) = node pair (8I + cn, 8J + rn) of the
+        // tile's 8 x 8 D block, cn = (lane & 15) >> 1, rn = (lane >> 5) + 2r:
+        // one 512-B load per table, then a lane permute per register
+        double dav[4], dbv[4];
+        spread_dblock(((const double*)(a.cbuf + CL.DAc))[(size_t)ti * 64 + lane], dav);
+        spread_dblock(((const double*)(a.cbuf + CL.DBc))[(size_t)ti * 64 + lane], dbv);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = 16 * J + (lane >> 4) + 4 * r;
+          acc[s][r] = -h_element<DYN, MEAS, HUBER>(a, Phi, Es, FtE, G, Cc[off + 64 * r], dav[r], dbv[r], row,
+                                                   col, Dm, LAM);
           if (BOUNDED && (ACT[row] | ACT[col])) acc[s][r] = 0.0;
         }
       } else {
@@ -783,19 +878,18 @@ __device__ __forceinline__ void build_tiles(const GnArgs& a, const ConstLayout& 
     const int ti = tile_index(J, J, a.NT);
     const size_t off = (size_t)ti * 256 + lane;
     const int col = 16 * J + (lane & 15);
-    double dac = 0.0, dbc = 0.0;
+    double dav[4], dbv[4];
     if constexpr (DYN::n == 2) {
-      dac = ((const double*)(a.cbuf + CL.DAc))[(size_t)ti * 64 + lane];
-      dbc = ((const double*)(a.cbuf + CL.DBc))[(size_t)ti * 64 + lane];
+      spread_dblock(((const double*)(a.cbuf + CL.DAc))[(size_t)ti * 64 + lane], dav);
+      spread_dblock(((const double*)(a.cbuf + CL.DBc))[(size_t)ti * 64 + lane], dbv);
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int tr = (lane >> 4) + 4 * r;
       double da, db;
       if constexpr (DYN::n == 2) {
-        const int src = (((lane & 15) >> 1) * 8 + (lane >> 5) + 2 * r) * 4;
-        da = bpermute_d(src, dac);
-        db = bpermute_d(src, dbc);
+        da = dav[r];
+        db = dbv[r];
       } else {
         da = DA[off + 64 * r];
         db = DB[off + 64 * r];
@@ -1292,6 +1386,7 @@ __global__ __launch_bounds__(NTHREADS, NW / 2) void k_gn(GnArgs a) {  // 2nd arg
     }
     if (it >= a.max_iter) break;
     build_tiles<DYN, MEAS, SLOTS, HUBER>(FA, FCL, FSL, sm, acc, wave, lane, stab);
+    DIAG_MARK(15);
     __syncthreads();
     DIAG_MARK(2);
     const bool ok = factor_forward<SLOTS>(FA, FSL, sm, acc, wave, lane, stab, DIAG_FARGS);
@@ -1577,7 +1672,10 @@ __global__ void k_build_cc(int P, int M, int n, int p, int NT, int has_prior, in
   ((double*)(cbuf + CL.DA))[(size_t)t * 256 + r * 64 + lane] = da;
   ((double*)(cbuf + CL.DB))[(size_t)t * 256 + r * 64 + lane] = db;
   if (r == 0) {
-    const int cn = lane >> 3, rn = lane & 7, l = 8 * I + cn, j = 8 * J + rn;
+    // lane (c + 16 g) holds node pair (cn, rn) = (c >> 1, (g >> 1) + 2 (2 (g & 1) + (c & 1))):
+    // the layout spread_dblock expects
+    const int cn = (lane & 15) >> 1, rn = (lane >> 5) + 2 * (2 * ((lane >> 4) & 1) + (lane & 1));
+    const int l = 8 * I + cn, j = 8 * J + rn;
     const bool ok = n == 2 && l < P && j < P;
     ((double*)(cbuf + CL.DAc))[(size_t)t * 64 + lane] = ok ? alpha * D[l * P + j] : 0.0;
     ((double*)(cbuf + CL.DBc))[(size_t)t * 64 + lane] = ok ? alpha * D[j * P + l] : 0.0;
