@@ -530,19 +530,25 @@ __global__ __launch_bounds__(256, 4) void k_big_assemble(BigArgs a) {
 //                 K = nb per tile visit, so every trailing tile is read and
 //                 written once per nb columns instead of once per 16 (the 16-wide
 //                 right-looking form moved ~4x the HBM bytes for the same flops).
-//                 L_J of four tile columns is staged in LDS (B operands, shared by
+//                 L_J of JB tile columns is staged in LDS (B operands, shared by
 //                 all waves); each wave walks tile rows I, holds L_I (A operands)
-//                 in registers and updates the row's (up to) four tiles.
+//                 in registers and updates the row's (up to) JB tiles.
 constexpr int BIG_KB = 8;      // tile columns per super-block
-constexpr int BIG_JB = 4;      // tile columns per LDS-staged trailing slab
+// Tile columns per LDS-staged trailing slab: every row visit reads its BIG_KB L_Ik
+// tiles once for JB output tiles, so the L traffic of the trailing update goes as
+// 1 / JB.  JB = 8 (128 KB slab, one workgroup per CU) for wide systems (NT >=
+// BIG_WIDE_NT, C4: HBM-bound there), JB = 4 (64 KB, two workgroups per CU, whose
+// overlap the latency-bound panel phase of narrower systems needs) otherwise.
+constexpr int BIG_WIDE_NT = 128;
 #ifndef MHE_BIG_KO
 #define MHE_BIG_KO 0  // knock-out mask for timing probes only (tools/ko_big.sh): 1 trailing, 2 in-block, 4 TRSM
 #endif
 constexpr int BIG_LB_TILES = BIG_KB * (BIG_KB - 1) / 2;
-constexpr int BIG_SLAB_TILES = BIG_JB * BIG_KB > BIG_LB_TILES ? BIG_JB * BIG_KB : BIG_LB_TILES;
-constexpr int BIG_CHOL_LDS = DTS + BIG_NW * 16 + 16 + 2 + BIG_SLAB_TILES * 256;  // doubles
+__host__ __device__ constexpr int big_slab_tiles(int JB) { return JB * BIG_KB > BIG_LB_TILES ? JB * BIG_KB : BIG_LB_TILES; }
+__host__ __device__ constexpr int big_chol_lds(int JB) { return DTS + BIG_NW * 16 + 16 + 2 + big_slab_tiles(JB) * 256; }  // doubles
 
-__global__ __launch_bounds__(BIG_NTHREADS, 4) void k_big_chol(BigArgs a) {
+template <int BIG_JB>
+__global__ __launch_bounds__(BIG_NTHREADS, BIG_JB == 8 ? 2 : 4) void k_big_chol(BigArgs a) {
   const int b = blockIdx.x;
   if (a.state[b] != BIG_RUNNING) return;
   const BigWs WL = big_ws_layout(a.P, a.M, a.n, a.NT, a.nz, a.nc);
@@ -652,58 +658,47 @@ __global__ __launch_bounds__(BIG_NTHREADS, 4) void k_big_chol(BigArgs a) {
       }
       __syncthreads();
       for (int I = J0 + wave; I < NT; I += BIG_NW) {
+        // row I of the slab: up to BIG_JB accumulators (jmax: the triangle's rows
+        // stop at the diagonal), L_Ik operands streamed one k tile ahead and read
+        // once per row visit
         const int jmax = min(jb, I - J0 + 1);
-        if (jmax == BIG_JB && kb == BIG_KB) {
-          // full row of the slab: BIG_JB accumulators, L_Ik operands streamed (one k tile ahead)
-          d4 c[BIG_JB];
+        d4 c[BIG_JB];
 #pragma unroll
-          for (int jj = 0; jj < BIG_JB; ++jj) {
+        for (int jj = 0; jj < BIG_JB; ++jj) {
+          if (jj < jmax) {
             const double* C = H + (size_t)big_tile_index(I, J0 + jj, NT) * 256;
 #pragma unroll
             for (int r = 0; r < 4; ++r) c[jj][r] = C[64 * r + lane];
           }
-          const double* LI0 = H + (size_t)big_tile_index(I, k0, NT) * 256;
-          double av[4];
+        }
+        const double* LI0 = H + (size_t)big_tile_index(I, k0, NT) * 256;
+        double av[4];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) av[r] = -LI0[64 * r + lane];
+        for (int r = 0; r < 4; ++r) av[r] = -LI0[64 * r + lane];
 #pragma unroll 1
-          for (int kk = 0; kk < BIG_KB; ++kk) {
-            double an[4];
-            const double* LIn = H + (size_t)big_tile_index(I, k0 + min(kk + 1, BIG_KB - 1), NT) * 256;
+        for (int kk = 0; kk < kb; ++kk) {
+          double an[4];
+          const double* LIn = H + (size_t)big_tile_index(I, k0 + min(kk + 1, kb - 1), NT) * 256;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) an[r] = -LIn[64 * r + lane];
+          for (int r = 0; r < 4; ++r) an[r] = -LIn[64 * r + lane];
 #pragma unroll
-            for (int jj = 0; jj < BIG_JB; ++jj) {
-              const double* Bt = LJ + (jj * BIG_KB + kk) * 256;
+          for (int jj = 0; jj < BIG_JB; ++jj) {
+            if (jj < jmax) {
+              const double* Bt = LJ + (jj * kb + kk) * 256;
 #pragma unroll
               for (int r = 0; r < 4; ++r)
                 c[jj] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[r], Bt[64 * r + lane], c[jj], 0, 0, 0);
             }
-#pragma unroll
-            for (int r = 0; r < 4; ++r) av[r] = an[r];
           }
 #pragma unroll
-          for (int jj = 0; jj < BIG_JB; ++jj) {
+          for (int r = 0; r < 4; ++r) av[r] = an[r];
+        }
+#pragma unroll
+        for (int jj = 0; jj < BIG_JB; ++jj) {
+          if (jj < jmax) {
             double* C = H + (size_t)big_tile_index(I, J0 + jj, NT) * 256;
 #pragma unroll
             for (int r = 0; r < 4; ++r) C[64 * r + lane] = c[jj][r];
-          }
-        } else {
-          // edge rows / last slab / short block: one tile at a time
-          for (int jj = 0; jj < jmax; ++jj) {
-            double* C = H + (size_t)big_tile_index(I, J0 + jj, NT) * 256;
-            d4 c;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) c[r] = C[64 * r + lane];
-            for (int kk = 0; kk < kb; ++kk) {
-              const double* LI = H + (size_t)big_tile_index(I, k0 + kk, NT) * 256;
-              const double* Bt = LJ + (jj * kb + kk) * 256;
-#pragma unroll
-              for (int r = 0; r < 4; ++r)
-                c = __builtin_amdgcn_mfma_f64_16x16x4f64(-LI[64 * r + lane], Bt[64 * r + lane], c, 0, 0, 0);
-            }
-#pragma unroll
-            for (int r = 0; r < 4; ++r) C[64 * r + lane] = c[r];
           }
         }
       }

@@ -1981,8 +1981,10 @@ struct LaunchBig {
   int run() {
     BigArgs& A = *a;
     const int npos = A.NTc * (A.NTc + 1) / 2;
-    const int smem = BIG_CHOL_LDS * (int)sizeof(double);
-    if (hipFuncSetAttribute((const void*)k_big_chol, hipFuncAttributeMaxDynamicSharedMemorySize, smem) != hipSuccess)
+    const bool wide = A.NT >= BIG_WIDE_NT;
+    const int smem = big_chol_lds(wide ? 8 : 4) * (int)sizeof(double);
+    if (hipFuncSetAttribute(wide ? (const void*)k_big_chol<8> : (const void*)k_big_chol<4>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, smem) != hipSuccess)
       return MHE_ERR_HIP;
     if (hipMemcpyAsync(A.X, X0, sizeof(double) * batch * A.P * A.n, hipMemcpyDeviceToDevice, st) != hipSuccess)
       return MHE_ERR_HIP;
@@ -2009,7 +2011,10 @@ struct LaunchBig {
       hipLaunchKernelGGL((k_big_resid<DYN, MEAS>), dim3(batch), dim3(BIG_NTHREADS), 0, st, A, 0);
       hipLaunchKernelGGL((k_big_assemble<DYN, MEAS>), dim3((npos * BigPairs<DYN::n>::NCH + 3) / 4, batch), dim3(256), 0,
                          st, A);
-      hipLaunchKernelGGL(k_big_chol, dim3(batch), dim3(BIG_NTHREADS), smem, st, A);
+      if (wide)
+        hipLaunchKernelGGL(k_big_chol<8>, dim3(batch), dim3(BIG_NTHREADS), smem, st, A);
+      else
+        hipLaunchKernelGGL(k_big_chol<4>, dim3(batch), dim3(BIG_NTHREADS), smem, st, A);
       if (K > 0) hipLaunchKernelGGL((k_big_border<DYN::n, MEAS::p>), dim3(batch), dim3(BIG_NTHREADS), smem_b, st, A);
       if (bounded)
         hipLaunchKernelGGL((k_big_linesearch<DYN, MEAS>), dim3(batch), dim3(BIG_NTHREADS), smem_ls, st, A);

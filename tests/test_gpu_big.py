@@ -124,3 +124,18 @@ def test_big_max_iter_zero_and_empty_batch():
     assert np.allclose(cost, cr, rtol=1e-12)
     X, cost, iters, status = s.solve(np.zeros((0, w.P, w.n)), w.U, np.zeros((0, w.M, w.p)), max_iter=3)
     assert X.shape == (0, w.P, w.n)
+
+
+def test_big_wide_slab_c4_shape_matches_oracle():
+    """The C4 shape (bicycle + pseudorange, N = 500, d = 3006, NT = 188 tile
+    columns) takes k_big_chol<8> (wide trailing slab, NT >= BIG_WIDE_NT)."""
+    w = configs.make_c4(B=1)
+    s = solver.from_workload(w)
+    assert s.large_system and w.P * w.n // 16 + 1 >= 128
+    pb = _problem(w)
+    X, cost, iters, status = _np(s.solve(w.X_init, w.U, w.Y, w.PAR, max_iter=2, tol=0.0))
+    Xr, cr, ir, sr = gn.gauss_newton(pb, w.X_init, _U(w), w.Y, _PAR(w), max_iter=2, tol=0.0)
+    k = _kappa(w, pb, Xr)
+    assert iters.tolist() == ir.tolist() and status.tolist() == sr.tolist()
+    assert np.abs(X - Xr).max() <= 1e-9 * k * (1 + np.abs(Xr).max())
+    assert np.allclose(cost, cr, rtol=1e-9 * k)
