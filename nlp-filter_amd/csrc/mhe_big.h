@@ -117,6 +117,11 @@ struct BigArgs {
   double* Z;         // (B, nz) current extra variables (Z_out)
   size_t tag_off;    // layout stamp of the constants buffer (mhe_build_constants)
   unsigned long long tag;
+  // component pairs (ca >= cb) of the measurement contraction, those whose G_e can be
+  // nonzero first ("live": both components in the measurement Jacobian's support),
+  // and the k_big_assemble chunking over them (BigPairPlan)
+  int npr, nlive, nchl, pchl, nch;
+  unsigned char pa[80], pb[80];
 };
 
 __device__ __forceinline__ int big_tile_index(int I, int J, int NT) { return J * NT - J * (J - 1) / 2 + (I - J); }
@@ -402,20 +407,55 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_resid(BigArgs a, int final
 // component pairs share the same operands Phi_E: one wave takes one tile position
 // (it >= jt) and a chunk of up to 8 pairs (ca >= cb) -- one MFMA accumulator per
 // pair -- so each K step of 4 epochs loads 2 Phi_E values (L2-resident, shared by
-// every trajectory) and feeds up to 8 MFMAs (G_e[ca][cb] read per lane; 8 accumulators keep ~4 waves/SIMD).  The
+// every trajectory) and feeds up to 8 MFMAs (G_e[ca][cb] read per lane; 8
+// accumulators keep ~4 waves/SIMD).  Pairs outside the measurement Jacobian's
+// support (BigGSupport) skip the GEMM: their chunks only write.  The
 // dynamics terms are added elementwise at the write; an off-diagonal pair also
 // writes the transposed tile (jt, it) from the same accumulator.
-template <int n>
-struct BigPairs {
-  static constexpr int NPR = n * (n + 1) / 2;
-  static constexpr int NCH = (NPR + 7) / 8;
-  static constexpr int PCH = (NPR + NCH - 1) / NCH;
+// State components a measurement row's Jacobian can touch (bit c: component c);
+// G_e[a][b] = sum H_i^T R_i H_i can be nonzero only when both bits are set.
+// Conservative (all components) unless the model says otherwise.
+template <class MEAS>
+struct BigGSupport {
+  static unsigned get(const int*, int n) { return (1u << n) - 1u; }
 };
+template <int N>
+struct BigGSupport<MeasPseudorange<N>> {  // h = |x[idx0..2] - sat| + x[idx3]
+  static unsigned get(const int* idx, int) { return 1u << idx[0] | 1u << idx[1] | 1u << idx[2] | 1u << idx[3]; }
+};
+
+constexpr int BIG_PCH = 8;  // pair accumulators per wave (4 waves / SIMD)
+
+// Pair table and chunking of k_big_assemble: the live pairs are split into
+// nchl chunks of <= pchl (balanced, <= BIG_PCH) that run the epoch GEMM; the
+// pairs whose contraction is zero (e.g. the clock-drift component under
+// pseudoranges) get chunks of BIG_PCH that only write the dynamics terms.
+inline void big_pair_plan(BigArgs& A, unsigned support) {
+  const int n = A.n;
+  int k = 0;
+  for (int pass = 0; pass < 2; ++pass)
+    for (int ca = 0; ca < n; ++ca)
+      for (int cb = 0; cb <= ca; ++cb) {
+        const bool live = (support >> ca & 1u) && (support >> cb & 1u);
+        if (live == (pass == 0)) {
+          A.pa[k] = (unsigned char)ca;
+          A.pb[k] = (unsigned char)cb;
+          ++k;
+        }
+      }
+  A.npr = k;
+  int nl = 0;
+  for (int ca = 0; ca < n; ++ca)
+    for (int cb = 0; cb <= ca; ++cb) nl += (support >> ca & 1u) && (support >> cb & 1u);
+  A.nlive = nl;
+  A.nchl = (nl + BIG_PCH - 1) / BIG_PCH;
+  A.pchl = A.nchl ? (nl + A.nchl - 1) / A.nchl : 0;
+  A.nch = A.nchl + (A.npr - nl + BIG_PCH - 1) / BIG_PCH;
+}
 
 template <class DYN, class MEAS>
 __global__ __launch_bounds__(256, 4) void k_big_assemble(BigArgs a) {
   constexpr int n = DYN::n, p = MEAS::p;
-  constexpr int NPR = BigPairs<n>::NPR, NCH = BigPairs<n>::NCH, PCH = BigPairs<n>::PCH;
   const int b = blockIdx.y;
   if (a.state[b] != BIG_RUNNING) return;
   const BigConst CL = big_const_layout(a.P, a.M, n, p, a.nc);
@@ -430,7 +470,7 @@ __global__ __launch_bounds__(256, 4) void k_big_assemble(BigArgs a) {
   const int E = a.M > 0 ? *(const int*)(a.cbuf + CL.ne) : 0;
   const int E4 = (E + 3) & ~3;  // K steps of 4 epochs (av = bv = 0 past E)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int NTc = a.NTc, P = a.P;
+  const int NTc = a.NTc, P = a.P, NCH = a.nch;
   const int npos = NTc * (NTc + 1) / 2;
   const int u = blockIdx.x * 4 + wave;
   if (u >= npos * NCH) return;
@@ -441,46 +481,38 @@ __global__ __launch_bounds__(256, 4) void k_big_assemble(BigArgs a) {
     ++it;
   }
   const int jt = pos;
-  d4 acc[PCH];
+  // this wave's pairs: table entries [q0, q0 + np) (BigPairPlan)
+  const bool live = ch < a.nchl;
+  const int q0 = live ? ch * a.pchl : a.nlive + (ch - a.nchl) * BIG_PCH;
+  const int np = min(live ? a.pchl : BIG_PCH, (live ? a.nlive : a.npr) - q0);
+  d4 acc[BIG_PCH];
 #pragma unroll
-  for (int q = 0; q < PCH; ++q) acc[q] = d4{0.0, 0.0, 0.0, 0.0};
+  for (int q = 0; q < BIG_PCH; ++q) acc[q] = d4{0.0, 0.0, 0.0, 0.0};
   const int row = 16 * it + (lane & 15), col = 16 * jt + (lane & 15);
   const bool vr = row < P, vc = col < P;
-  const int p0 = ch * PCH;
-  int ca = 0, cb = p0;  // first pair of the chunk
-  while (cb > ca) {
-    cb -= ca + 1;
-    ++ca;
-  }
-  int goff[PCH];        // offsets of G_e[ca][cb] for the chunk's pairs
-  {
-    int x = ca, y = cb;
-#pragma unroll
-    for (int q = 0; q < PCH; ++q) {
-      goff[q] = x * n + y;
-      if (++y > x) {
-        y = 0;
-        ++x;
-      }
-    }
-  }
   const double* Ge = ws + WL.Ge;
-  for (int e0 = 0; e0 < E4; e0 += 4) {
-    const int e = e0 + (lane >> 4);
-    double av = 0.0, bv = 0.0;
-    const int ec = e < E ? e : E - 1;
-    if (e < E) {
-      av = vr ? PhiE[(size_t)e * P + row] : 0.0;
-      bv = vc ? PhiE[(size_t)e * P + col] : 0.0;
-    }
-    const double* gp = Ge + (size_t)ec * n * n;
+  if (live) {
+    int goff[BIG_PCH];  // offsets of G_e[ca][cb] for the chunk's pairs
 #pragma unroll
-    for (int q = 0; q < PCH; ++q)
-      if (p0 + q < NPR) acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av * gp[goff[q]], bv, acc[q], 0, 0, 0);
+    for (int q = 0; q < BIG_PCH; ++q) goff[q] = q < np ? a.pa[q0 + q] * n + a.pb[q0 + q] : 0;
+    for (int e0 = 0; e0 < E4; e0 += 4) {
+      const int e = e0 + (lane >> 4);
+      double av = 0.0, bv = 0.0;
+      const int ec = e < E ? e : E - 1;
+      if (e < E) {
+        av = vr ? PhiE[(size_t)e * P + row] : 0.0;
+        bv = vc ? PhiE[(size_t)e * P + col] : 0.0;
+      }
+      const double* gp = Ge + (size_t)ec * n * n;
+#pragma unroll
+      for (int q = 0; q < BIG_PCH; ++q)
+        if (q < np) acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av * gp[goff[q]], bv, acc[q], 0, 0, 0);
+    }
   }
 #pragma unroll
-  for (int q = 0; q < PCH; ++q) {
-    if (p0 + q < NPR) {
+  for (int q = 0; q < BIG_PCH; ++q) {
+    if (q < np) {
+      const int ca = a.pa[q0 + q], cb = a.pb[q0 + q];
       const double qab = a.alpha * a.alpha * Qw[ca * n + cb];
       // tile (it, jt) of block (ca, cb) and, off the diagonal pair, its transpose into (jt, it)
 #pragma unroll
@@ -512,10 +544,6 @@ __global__ __launch_bounds__(256, 4) void k_big_assemble(BigArgs a) {
           tile[tr * 16 + tc] = v;
         }
       }
-    }
-    if (++cb > ca) {
-      cb = 0;
-      ++ca;
     }
   }
 }

@@ -1981,6 +1981,7 @@ struct LaunchBig {
   int run() {
     BigArgs& A = *a;
     const int npos = A.NTc * (A.NTc + 1) / 2;
+    big_pair_plan(A, BigGSupport<MEAS>::get(A.idx, A.n));
     const bool wide = A.NT >= BIG_WIDE_NT;
     const int smem = big_chol_lds(wide ? 8 : 4) * (int)sizeof(double);
     if (hipFuncSetAttribute(wide ? (const void*)k_big_chol<8> : (const void*)k_big_chol<4>,
@@ -2009,7 +2010,7 @@ struct LaunchBig {
     }
     for (int it = 0; it < max_iter; ++it) {
       hipLaunchKernelGGL((k_big_resid<DYN, MEAS>), dim3(batch), dim3(BIG_NTHREADS), 0, st, A, 0);
-      hipLaunchKernelGGL((k_big_assemble<DYN, MEAS>), dim3((npos * BigPairs<DYN::n>::NCH + 3) / 4, batch), dim3(256), 0,
+      hipLaunchKernelGGL((k_big_assemble<DYN, MEAS>), dim3((npos * A.nch + 3) / 4, batch), dim3(256), 0,
                          st, A);
       if (wide)
         hipLaunchKernelGGL(k_big_chol<8>, dim3(batch), dim3(BIG_NTHREADS), smem, st, A);
