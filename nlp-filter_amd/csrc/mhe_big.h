@@ -405,10 +405,10 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_resid(BigArgs a, int final
 //   + M_ab,   M_ab = Phi_E^T diag(G_ab) Phi_E   (G_e = sum_{i in e} H_i^T R_i H_i)
 // M_ab is a GEMM over the E epochs, symmetric (M_ab = M_ab^T = M_ba), and all
 // component pairs share the same operands Phi_E: one wave takes one tile position
-// (it >= jt) and a chunk of up to 8 pairs (ca >= cb) -- one MFMA accumulator per
+// (it >= jt) and a chunk of up to BIG_PCH pairs (ca >= cb) -- one MFMA accumulator per
 // pair -- so each K step of 4 epochs loads 2 Phi_E values (L2-resident, shared by
-// every trajectory) and feeds up to 8 MFMAs (G_e[ca][cb] read per lane; 8
-// accumulators keep ~4 waves/SIMD).  Pairs outside the measurement Jacobian's
+// every trajectory) and feeds up to 5 MFMAs (G_e[ca][cb] read per lane; 5
+// accumulators: 96 VGPRs, no spills).  Pairs outside the measurement Jacobian's
 // support (BigGSupport) skip the GEMM: their chunks only write.  The
 // dynamics terms are added elementwise at the write; an off-diagonal pair also
 // writes the transposed tile (jt, it) from the same accumulator.
@@ -424,7 +424,7 @@ struct BigGSupport<MeasPseudorange<N>> {  // h = |x[idx0..2] - sat| + x[idx3]
   static unsigned get(const int* idx, int) { return 1u << idx[0] | 1u << idx[1] | 1u << idx[2] | 1u << idx[3]; }
 };
 
-constexpr int BIG_PCH = 8;  // pair accumulators per wave (4 waves / SIMD)
+constexpr int BIG_PCH = 5;  // pair accumulators per wave (96 VGPRs, no spills)
 
 // Pair table and chunking of k_big_assemble: the live pairs are split into
 // nchl chunks of <= pchl (balanced, <= BIG_PCH) that run the epoch GEMM; the
