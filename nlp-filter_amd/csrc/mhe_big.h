@@ -495,18 +495,31 @@ __global__ __launch_bounds__(256, 4) void k_big_assemble(BigArgs a) {
     int goff[BIG_PCH];  // offsets of G_e[ca][cb] for the chunk's pairs
 #pragma unroll
     for (int q = 0; q < BIG_PCH; ++q) goff[q] = q < np ? a.pa[q0 + q] * n + a.pb[q0 + q] : 0;
-    for (int e0 = 0; e0 < E4; e0 += 4) {
+    // K steps of 4 epochs, software-pipelined: step e0 + 4's Phi_E and G_e loads are
+    // issued before step e0's MFMAs (clamped reads; padding epochs / rows zeroed)
+    double av, bv, gv[BIG_PCH];
+    auto issue = [&](int e0) {
       const int e = e0 + (lane >> 4);
-      double av = 0.0, bv = 0.0;
       const int ec = e < E ? e : E - 1;
-      if (e < E) {
-        av = vr ? PhiE[(size_t)e * P + row] : 0.0;
-        bv = vc ? PhiE[(size_t)e * P + col] : 0.0;
-      }
+      av = PhiE[(size_t)ec * P + (vr ? row : 0)];
+      bv = PhiE[(size_t)ec * P + (vc ? col : 0)];
+      if (!(e < E && vr)) av = 0.0;
+      if (!(e < E && vc)) bv = 0.0;
       const double* gp = Ge + (size_t)ec * n * n;
 #pragma unroll
+      for (int q = 0; q < BIG_PCH; ++q) gv[q] = gp[goff[q]];
+    };
+    issue(0);
+#pragma unroll 1
+    for (int e0 = 0; e0 < E4; e0 += 4) {
+      const double a0 = av, b0 = bv;
+      double g0[BIG_PCH];
+#pragma unroll
+      for (int q = 0; q < BIG_PCH; ++q) g0[q] = gv[q];
+      if (e0 + 4 < E4) issue(e0 + 4);
+#pragma unroll
       for (int q = 0; q < BIG_PCH; ++q)
-        if (q < np) acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av * gp[goff[q]], bv, acc[q], 0, 0, 0);
+        if (q < np) acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0 * g0[q], b0, acc[q], 0, 0, 0);
     }
   }
 #pragma unroll
