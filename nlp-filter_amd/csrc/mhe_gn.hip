@@ -956,6 +956,23 @@ __device__ __forceinline__ double row16_sum(double v) {
   return v;
 }
 
+// Sums over the 16 lanes of a DPP row of four values at once: lane (c, g) ends with
+// sum over its row of v[r], r = 2 (c >> 3) + ((c >> 2) & 1) (replicated over c & 3).
+// The first two steps exchange half of the remaining values (row_ror:8 pairs c with
+// c ^ 8, row_half_mirror c with 7 - c inside each half), the last two are plain
+// butterflies: 6 DPP moves and 4 adds instead of 4 row16_sum's 16 and 16.
+__device__ __forceinline__ double row16_sum4(const double (&v)[4], int c) {
+  const bool b3 = c & 8, b2 = c & 4;
+  const double k0 = b3 ? v[2] : v[0], k1 = b3 ? v[3] : v[1];
+  const double s0 = b3 ? v[0] : v[2], s1 = b3 ? v[1] : v[3];
+  const double w0 = k0 + dpp_d<0x128>(s0), w1 = k1 + dpp_d<0x128>(s1);  // row_ror:8
+  const double k = b2 ? w1 : w0, t = b2 ? w0 : w1;
+  double x = k + dpp_d<0x141>(t);  // row_half_mirror
+  x += dpp_d<0x1B>(x);             // quad_perm [3,2,1,0]
+  x += dpp_d<0xB1>(x);             // quad_perm [1,0,3,2]
+  return x;
+}
+
 // 1/sqrt(x) for a positive finite pivot: hardware v_rsq_f64 (~1e-9 relative)
 // refined by one Newton step (error squared: ~1 ulp).  Non-positive or
 // non-finite pivots are flagged by the caller and poison the factor anyway.
@@ -1236,14 +1253,14 @@ __device__ __forceinline__ void backward(const GnArgs& a, const SmemLayout& SL, 
       const int I = IJ & 0xffff, J = IJ >> 16;
       if (IJ >= 0 && I == bb && (!KO(6) || J == bb - 1)) {
         const bool crit = J == bb - 1;
-        if (crit) __builtin_amdgcn_s_setprio(3);
         double* yj = DV + 16 * J;
         const int g = lane_o >> 4, c = lane_o & 15;
-        double part[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) part[r] = row16_sum(acc[s][r] * db);
-        // lane l of row group g = l>>4 holds the sums for rows g + 4r
         if (crit) {
+          __builtin_amdgcn_s_setprio(3);
+          double part[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) part[r] = row16_sum(acc[s][r] * db);
+          // lane l of row group g = l>>4 holds the sums for rows g + 4r
           // delta_J = L_JJ^-T (y_J - U_{J,bb} delta_bb) straight from these registers:
           // lane (c, g) takes the rows g + 4r it already holds, rows4_sum completes the
           // dot -- no store / reload of y_J in between
@@ -1255,10 +1272,10 @@ __device__ __forceinline__ void backward(const GnArgs& a, const SmemLayout& SL, 
           if (lane_o < 16) yj[c] = dv;  // every lane has read y_J (rows4_sum depends on all of them)
           __builtin_amdgcn_s_setprio(0);
         } else {
-          // lane (l & 15) == r writes row g + 4r
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (c == r) yj[g + 4 * r] -= part[r];
+          // the four row sums at once (row16_sum4): lane (c, g) holds row g + 4 r(c)'s
+          const double v[4] = {acc[s][0] * db, acc[s][1] * db, acc[s][2] * db, acc[s][3] * db};
+          const double z = row16_sum4(v, c);
+          if ((c & 3) == 0) yj[g + 4 * (2 * (c >> 3) + ((c >> 2) & 1))] -= z;
         }
       }
     }
