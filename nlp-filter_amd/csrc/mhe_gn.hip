@@ -1068,6 +1068,9 @@ __device__ __forceinline__ bool factor_forward(const GnArgs& a, const SmemLayout
     // ---- T(k): U_kb = L_kk^-1 A_kb for the tiles (k, b) of this wave, slots [sT, sU)
     const int sT = slot_start(k < 0 ? 0 : k, wave_o, NT), sU = slot_start(k + 1, wave_o, NT);
     const int nS = slot_start(NT - 1, wave_o, NT);
+    // the slot ranges [sT, sU) and [sU, nS) as wave-uniform bit masks: one bit test
+    // per unrolled slot instead of two compares and their combination
+    const unsigned mT = (1u << sU) - (1u << sT), mU = (1u << nS) - (1u << sU);
     if (k >= 0 && wave_o == (k + 2) % NW)  // forward solve, one block behind the factorization
       block_fwd(DT + k * DTS, BV + 16 * k, YV + 16 * k, lane_o);
     if (k >= 0) {
@@ -1077,7 +1080,7 @@ __device__ __forceinline__ bool factor_forward(const GnArgs& a, const SmemLayout
       for (int r = 0; r < 4; ++r) la[r] = -LT[(4 * r + (lane_o >> 4)) * LIS + (lane_o & 15)];  // -L^-1[l&15][4r+(l>>4)]
 #pragma unroll
       for (int s = 0; s < SLOTS; ++s) {
-        if (s >= sT && s < sU) {
+        if ((mT >> s) & 1u) {
           d4 u = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
           for (int r = 0; r < 4; ++r) u = __builtin_amdgcn_mfma_f64_16x16x4f64(la[r], acc[s][r], u, 0, 0, 0);
@@ -1134,7 +1137,7 @@ __device__ __forceinline__ bool factor_forward(const GnArgs& a, const SmemLayout
     if (k >= 0 && !KO(1)) {
 #pragma unroll
       for (int s = 0; s < SLOTS; ++s) {
-        if (s >= sU && s < nS) {
+        if ((mU >> s) & 1u) {
           const int IJ = slot_ij(stab_o, s);
           const double* ua = PB + ((IJ >> 16) - k - 1) * 256 + lane_o;
           const double* ub = PB + ((IJ & 0xffff) - k - 1) * 256 + lane_o;
