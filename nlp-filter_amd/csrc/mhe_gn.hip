@@ -72,7 +72,7 @@ __host__ __device__ inline ConstLayout const_layout(int P, int M, int n, int p, 
 }
 
 struct SmemLayout {  // offsets in doubles
-  int Xs, Vs, FtV, Es, FtE, GE, G, LAM, BV, YV, PB, DT, RED, XO, ACT, total;
+  int Xs, Vs, FtV, Es, FtE, GE, G, LAM, BV, YV, PB, DT, RED, ROWM, XO, ACT, total;
 };
 
 __host__ __device__ inline int rnd2(int x) { return (x + 1) & ~1; }  // keep 16-B alignment
@@ -97,6 +97,7 @@ __host__ __device__ inline SmemLayout smem_layout(int P, int M, int n, int NT, b
   S.PB = o;   o += (NT - 1) * 256;      // block row k of U (tiles U_kb, b > k), register order
   S.DT = o;   o += NT * DTS;            // diagonal blocks
   S.RED = o;  o += 4 * NW + 8;
+  S.ROWM = o; o += NW * 8;              // per wave, per block row I: bit mask of its slots (I, J)
   // bounded problems only (projected Newton, k_gn<..., BOUNDED>): the iterate the
   // line search starts from, and the epsilon-active set (one int per unknown)
   S.XO = o;   o += bounded ? rnd2(P * n) : 0;
@@ -296,6 +297,19 @@ __device__ __forceinline__ int slot_ij(int stab, int s) { return __builtin_amdgc
 __device__ __forceinline__ int slot_start(int j, int wave, int NT) {
   const int base = j * (NT - 1) - j * (j - 1) / 2;  // tiles in columns < j
   return base > wave ? (base - wave + NW - 1) / NW : 0;
+}
+
+// Per wave and block row I (< 16): the bit mask of the wave's slots holding a tile
+// (I, J), written once per launch (the backward solve tests one bit per slot
+// instead of decoding every slot's coordinates at every block step).
+__device__ __forceinline__ void init_rowmask(int* rowm, int wave, int lane, int stab) {
+  unsigned m = 0;
+#pragma unroll
+  for (int s = 0; s < MAX_SLOTS; ++s) {
+    const int IJ = slot_ij(stab, s);
+    if (IJ >= 0 && (IJ & 0xffff) == lane) m |= 1u << s;
+  }
+  if (lane < 16) rowm[wave * 16 + lane] = (int)m;
 }
 
 // ------------------------------------------------------------ model phases
@@ -1248,13 +1262,15 @@ __device__ __forceinline__ void backward(const GnArgs& a, const SmemLayout& SL, 
     asm volatile("" : "+v"(lane_o));
     asm volatile("" : "+v"(stab_o));
     const double db = DV[16 * bb + (lane_o & 15)];
+    const unsigned rm = __builtin_amdgcn_readfirstlane(((const int*)(sm + SL.ROWM))[wave * 16 + bb]);
     // slots in DESCENDING order: within row bb the tile (bb, bb-1) has the largest
     // column-major index, and its owner's delta_{bb-1} is the critical chain
 #pragma unroll
     for (int s = SLOTS - 1; s >= 0; --s) {
+      if (!((rm >> s) & 1u)) continue;
       const int IJ = slot_ij(stab_o, s);
-      const int I = IJ & 0xffff, J = IJ >> 16;
-      if (IJ >= 0 && I == bb && (!KO(6) || J == bb - 1)) {
+      const int J = IJ >> 16;
+      if (!KO(6) || J == bb - 1) {
         const bool crit = J == bb - 1;
         double* yj = DV + 16 * J;
         const int g = lane_o >> 4, c = lane_o & 15;
@@ -1328,6 +1344,7 @@ __global__ __launch_bounds__(NTHREADS, NW / 2) void k_gn(GnArgs a) {  // 2nd arg
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int b = blockIdx.x;
   const int stab = make_slot_table(wave, lane, a.NT);
+  init_rowmask((int*)(sm + SL.ROWM), wave, lane, stab);
   double* Xs = sm + SL.Xs;
   if (threadIdx.x == 0) *(int*)(sm + SL.RED + 4 * NW) = 0;  // NOT_SPD flag
   double* DV = sm + SL.YV;  // delta after backward()
@@ -1523,6 +1540,7 @@ __global__ __launch_bounds__(NTHREADS, NW / 2) void k_gn_bounded(GnArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int b = blockIdx.x;
   const int stab = make_slot_table(wave, lane, a.NT);
+  init_rowmask((int*)(sm + SL.ROWM), wave, lane, stab);
   double* Xs = sm + SL.Xs;
   double* XO = sm + SL.XO;
   int* ACT = (int*)(sm + SL.ACT);
