@@ -987,6 +987,40 @@ __device__ __forceinline__ double row16_sum4(const double (&v)[4], int c) {
   return x;
 }
 
+// acc += (src0 of lane j of this 16-lane row) * src1: v_fmac_f64 with a DPP64
+// row_newbcast source (one instruction; the compiler does not fuse a v_mov_b64_dpp
+// into an f64 fma itself).  ISA hazard: a DPP source must not have been written by
+// the two previous VALU instructions.  The first use after src0 was written
+// (`fresh`) carries the wait states and passes src0 through as an output, so every
+// later use depends on it and cannot be scheduled in front of it.
+#define MHE_FMAC_BCAST(J)                                                                                  \
+  case J:                                                                                                  \
+    if (fresh)                                                                                             \
+      asm("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:" #J " row_mask:0xf bank_mask:0xf"           \
+          : "+v"(acc), "+v"(src0) : "v"(src1));                                                            \
+    else                                                                                                   \
+      asm("v_fmac_f64_dpp %0, %1, %2 row_newbcast:" #J " row_mask:0xf bank_mask:0xf"                        \
+          : "+v"(acc) : "v"(src0), "v"(src1));                                                             \
+    break;
+__device__ __forceinline__ void fmac_rowbcast(double& acc, double& src0, double src1, int j, bool fresh) {
+  switch (j) {
+    MHE_FMAC_BCAST(1) MHE_FMAC_BCAST(2) MHE_FMAC_BCAST(3) MHE_FMAC_BCAST(4) MHE_FMAC_BCAST(5)
+    MHE_FMAC_BCAST(6) MHE_FMAC_BCAST(7) MHE_FMAC_BCAST(8) MHE_FMAC_BCAST(9) MHE_FMAC_BCAST(10)
+    MHE_FMAC_BCAST(11) MHE_FMAC_BCAST(12) MHE_FMAC_BCAST(13) MHE_FMAC_BCAST(14) MHE_FMAC_BCAST(15)
+    default: break;
+  }
+}
+#undef MHE_FMAC_BCAST
+
+// The value of the first 16-lane row (lanes 0..15) in the first two rows: element
+// [0] of v_permlane16_swap with the same register as both operands.
+__device__ __forceinline__ double row0_both(double v) {
+  const long long b = __double_as_longlong(v);
+  const auto l = __builtin_amdgcn_permlane16_swap((int)b, (int)b, false, false);
+  const auto h = __builtin_amdgcn_permlane16_swap((int)(b >> 32), (int)(b >> 32), false, false);
+  return __longlong_as_double(((long long)h[0] << 32) | (unsigned int)l[0]);
+}
+
 // 1/sqrt(x) for a positive finite pivot: hardware v_rsq_f64 (~1e-9 relative)
 // refined by one Newton step (error squared: ~1 ulp).  Non-positive or
 // non-finite pivots are flagged by the caller and poison the factor anyway.
@@ -1033,8 +1067,14 @@ __device__ __forceinline__ bool panel(double* DTk, int lane) {
     bad |= !(piv > 0.0 && piv < INFINITY);
     const double q = v[c] * rsqrt_pivot(piv);
     v[c] = q;
+    if (c < 15) {
+      // L column c (the row lanes' q) into both 16-lane rows, then for j > c
+      // v[j] -= L_jc q with L_jc broadcast from lane j of the row by the fma itself
+      double lq = row0_both(q);
+      const double nq = -q;
 #pragma unroll
-    for (int j = c + 1; j < 16; ++j) v[j] -= q * readlane_d(q, j);
+      for (int j = c + 1; j < 16; ++j) fmac_rowbcast(v[j], lq, nq, j, j == c + 1);
+    }
   }
   if (erow) {
 #pragma unroll
