@@ -586,7 +586,7 @@ constexpr int BIG_WIDE_NT = 128;
 #endif
 constexpr int BIG_LB_TILES = BIG_KB * (BIG_KB - 1) / 2;
 __host__ __device__ constexpr int big_slab_tiles(int JB) { return JB * BIG_KB > BIG_LB_TILES ? JB * BIG_KB : BIG_LB_TILES; }
-__host__ __device__ constexpr int big_chol_lds(int JB) { return DTS + BIG_NW * 16 + 16 + 2 + big_slab_tiles(JB) * 256; }  // doubles
+__host__ __device__ constexpr int big_chol_lds(int JB) { return DTS + BIG_NW * 16 + 16 + 2 + UNITS + big_slab_tiles(JB) * 256; }  // doubles
 
 template <int BIG_JB>
 __global__ __launch_bounds__(BIG_NTHREADS, BIG_JB == 8 ? 2 : 4) void k_big_chol(BigArgs a) {
@@ -599,14 +599,16 @@ __global__ __launch_bounds__(BIG_NTHREADS, BIG_JB == 8 ? 2 : 4) void k_big_chol(
   double* BV = ws + WL.BV;
   double* YV = ws + WL.YV;
   extern __shared__ __attribute__((aligned(16))) double sm[];
-  double* DT = sm;                 // DTS: -A_kk, then L_kk^-T
+  double* DT = sm;                 // DTS: A_kk, then L_kk^-T
   double* PART = sm + DTS;         // BIG_NW x 16 partial sums (backward)
   double* YL = PART + BIG_NW * 16; // 16: block right-hand side (backward)
   int* flag = (int*)(YL + 16);
-  double* LJ = sm + DTS + BIG_NW * 16 + 16 + 2;  // staged L_Jk tiles [jj][kk][256], row-major
+  double* UN = sm + DTS + BIG_NW * 16 + 16 + 2;  // identity rows for the panel (unit_row)
+  double* LJ = UN + UNITS;                        // staged L_Jk tiles [jj][kk][256], row-major
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int NT = a.NT;
   if (threadIdx.x == 0) *flag = 0;
+  init_units(UN);
   for (int k0 = 0; k0 < NT; k0 += BIG_KB) {
     const int kend = min(k0 + BIG_KB, NT);
     // ---- panel phase, left-looking inside the block column: at step k every tile
@@ -618,7 +620,7 @@ __global__ __launch_bounds__(BIG_NTHREADS, BIG_JB == 8 ? 2 : 4) void k_big_chol(
     for (int k = k0; k < kend; ++k) {
       const int nk = k - k0;
       if (wave == 0) {
-        // diagonal tile: A_kk - sum L_kk' L_kk'^T -> DT (negated), panel, y_k
+        // diagonal tile: A_kk - sum L_kk' L_kk'^T -> DT, panel, y_k
         const double* Akk = H + (size_t)big_tile_index(k, k, NT) * 256;
         d4 c;
 #pragma unroll
@@ -632,9 +634,9 @@ __global__ __launch_bounds__(BIG_NTHREADS, BIG_JB == 8 ? 2 : 4) void k_big_chol(
           }
         }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) DT[64 * r + lane] = -c[r];
+        for (int r = 0; r < 4; ++r) DT[64 * r + lane] = c[r];
         wave_lds_sync();
-        const bool bad = panel(DT, lane);
+        const bool bad = panel(DT, UN, lane);
         if (bad && lane == 0) *flag = 1;
         wave_lds_sync();
         block_fwd(DT, BV + 16 * k, YV + 16 * k, lane);  // y_k = L_kk^-1 b_k

@@ -72,13 +72,19 @@ __host__ __device__ inline ConstLayout const_layout(int P, int M, int n, int p, 
 }
 
 struct SmemLayout {  // offsets in doubles
-  int Xs, Vs, FtV, Es, FtE, GE, G, LAM, BV, YV, PB, DT, RED, ROWM, XO, ACT, total;
+  int Xs, Vs, FtV, Es, FtE, GE, G, LAM, BV, YV, PB, DT, RED, ROWM, UN, XO, ACT, total;
 };
 
 __host__ __device__ inline int rnd2(int x) { return (x + 1) & ~1; }  // keep 16-B alignment
 
 constexpr int DTS = 272;  // diagonal-tile stride: A_kk row-major (256), then L_kk^-T with row stride 17
 constexpr int LIS = 17;   // row stride of L_kk^-T (conflict-free row and column reads)
+// Two unit vectors, e_16 in [0, 34) and e_51 in [34, 68): row i of the 16 x 16 identity
+// is 16 consecutive doubles at an even (16-B aligned) offset, unit_row(i) (panel).
+constexpr int UNITS = 68;
+// blgp of v_mfma_f64 on gfx950 = neg modifiers [A, B, C]: bit 0 negates A
+constexpr int MFMA_NEG_A = 1;
+__host__ __device__ constexpr int unit_row(int i) { return (i & 1) ? 51 - i : 16 - i; }
 
 __host__ __device__ inline SmemLayout smem_layout(int P, int M, int n, int NT, bool nonlinear, bool bounded = false) {
   SmemLayout S;
@@ -98,6 +104,7 @@ __host__ __device__ inline SmemLayout smem_layout(int P, int M, int n, int NT, b
   S.DT = o;   o += NT * DTS;            // diagonal blocks
   S.RED = o;  o += 4 * NW + 8;
   S.ROWM = o; o += NW * 8;              // per wave, per block row I: bit mask of its slots (I, J)
+  S.UN = o;   o += UNITS;               // identity rows for the panel (unit_row)
   // bounded problems only (projected Newton, k_gn<..., BOUNDED>): the iterate the
   // line search starts from, and the epsilon-active set (one int per unknown)
   S.XO = o;   o += bounded ? rnd2(P * n) : 0;
@@ -302,6 +309,13 @@ __device__ __forceinline__ int slot_start(int j, int wave, int NT) {
 // Per wave and block row I (< 16): the bit mask of the wave's slots holding a tile
 // (I, J), written once per launch (the backward solve tests one bit per slot
 // instead of decoding every slot's coordinates at every block step).
+// the unit vectors behind unit_row, written by wave 0 alone (the big path's panel
+// runs on wave 0 before any workgroup barrier)
+__device__ __forceinline__ void init_units(double* un) {
+  if (threadIdx.x < 64)
+    for (int e = threadIdx.x; e < UNITS; e += 64) un[e] = (e == 16 || e == 51) ? 1.0 : 0.0;
+}
+
 __device__ __forceinline__ void init_rowmask(int* rowm, int wave, int lane, int stab) {
   unsigned m = 0;
 #pragma unroll
@@ -908,7 +922,7 @@ __device__ __forceinline__ void build_tiles(const GnArgs& a, const ConstLayout& 
         da = DA[off + 64 * r];
         db = DB[off + 64 * r];
       }
-      double v = -h_element<DYN, MEAS, HUBER>(a, Phi, Es, FtE, G, Cc[off + 64 * r], da, db, 16 * J + tr, col, Dm, LAM);
+      double v = h_element<DYN, MEAS, HUBER>(a, Phi, Es, FtE, G, Cc[off + 64 * r], da, db, 16 * J + tr, col, Dm, LAM);
       if (BOUNDED && (ACT[16 * J + tr] | ACT[col]) && 16 * J + tr != col) v = 0.0;
       DT[J * DTS + tr * 16 + (lane & 15)] = v;
     }
@@ -940,7 +954,7 @@ __device__ __forceinline__ void load_tiles(const GnArgs& a, const SmemLayout& SL
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int tr = (lane >> 4) + 4 * r;
-      DT[J * DTS + tr * 16 + (lane & 15)] = -Hb[(size_t)(16 * J + tr) * dp + 16 * J + (lane & 15)];
+      DT[J * DTS + tr * 16 + (lane & 15)] = Hb[(size_t)(16 * J + tr) * dp + 16 * J + (lane & 15)];
     }
 }
 
@@ -987,7 +1001,7 @@ __device__ __forceinline__ double row16_sum4(const double (&v)[4], int c) {
   return x;
 }
 
-// acc += (src0 of lane j of this 16-lane row) * src1: v_fmac_f64 with a DPP64
+// acc -= (src0 of lane j of this 16-lane row) * src1: v_fmac_f64 with a negated DPP64
 // row_newbcast source (one instruction; the compiler does not fuse a v_mov_b64_dpp
 // into an f64 fma itself).  ISA hazard: a DPP source must not have been written by
 // the two previous VALU instructions.  The first use after src0 was written
@@ -996,13 +1010,13 @@ __device__ __forceinline__ double row16_sum4(const double (&v)[4], int c) {
 #define MHE_FMAC_BCAST(J)                                                                                  \
   case J:                                                                                                  \
     if (fresh)                                                                                             \
-      asm("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:" #J " row_mask:0xf bank_mask:0xf"           \
+      asm("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %2 row_newbcast:" #J " row_mask:0xf bank_mask:0xf"          \
           : "+v"(acc), "+v"(src0) : "v"(src1));                                                            \
     else                                                                                                   \
-      asm("v_fmac_f64_dpp %0, %1, %2 row_newbcast:" #J " row_mask:0xf bank_mask:0xf"                        \
+      asm("v_fmac_f64_dpp %0, -%1, %2 row_newbcast:" #J " row_mask:0xf bank_mask:0xf"                       \
           : "+v"(acc) : "v"(src0), "v"(src1));                                                             \
     break;
-__device__ __forceinline__ void fmac_rowbcast(double& acc, double& src0, double src1, int j, bool fresh) {
+__device__ __forceinline__ void fnmac_rowbcast(double& acc, double& src0, double src1, int j, bool fresh) {
   switch (j) {
     MHE_FMAC_BCAST(1) MHE_FMAC_BCAST(2) MHE_FMAC_BCAST(3) MHE_FMAC_BCAST(4) MHE_FMAC_BCAST(5)
     MHE_FMAC_BCAST(6) MHE_FMAC_BCAST(7) MHE_FMAC_BCAST(8) MHE_FMAC_BCAST(9) MHE_FMAC_BCAST(10)
@@ -1031,56 +1045,54 @@ __device__ __forceinline__ double rsqrt_pivot(double x) {
 }
 
 // Panel of block k, run by ONE wave (look-ahead: during the previous step's
-// trailing update).  On entry DT[k] holds the fully updated A_kk (row-major,
-// negated as all tiles).  One right-looking elimination in which the same
-// register index j carries two things, one per lane role:
+// trailing update).  On entry DT[k] holds the fully updated A_kk (row-major).
+// One right-looking elimination in which the same register index j carries two
+// things, one per lane role:
 //   lanes  0..15  row i of A_kk:              v[j] = A'_ij
-//   lanes 16..31  column t of the identity:   v[j] = E'_jt
+//   lanes 16..31  column t of the identity:   v[j] = E'_jt  (loaded from UN)
 // Pivot c:  rs = 1 / sqrt(A'_cc);  q = v[c] rs  (= L_ic on row lanes, = (L^-1)_ct
 // on the others, final at that point);  then for j > c
-//   v[j] -= q L_jc   with L_jc = q of row lane j (v_readlane),
+//   v[j] -= L_jc q   with L_jc = q of row lane j,
 // i.e. ONE fma updates the Cholesky trailing row and the forward substitution
-// L Y = I together (~550 VALU instructions, ~40 VGPRs).  Stores L_kk^-T into
-// DT[k] (row stride LIS).  The right-hand side is NOT carried here: y_k =
-// L_kk^-1 b_k is formed later by another wave (off this critical chain).
-// Returns true if a pivot was not positive and finite (wave-uniform).
-__device__ __forceinline__ bool panel(double* DTk, int lane) {
+// L Y = I together: a v_fmac_f64 whose DPP64 row_newbcast source broadcasts L_jc
+// from lane j of the row (the L column reaches the identity lanes' row by one
+// v_permlane16_swap per pivot).  ~450 instructions, the wave's issue rate bounds it
+// (every instruction counts, whatever its kind).  Stores L_kk^-T into DT[k] (row
+// stride LIS).  The right-hand side is NOT carried here: y_k = L_kk^-1 b_k is formed
+// later by another wave (off this critical chain).
+// Returns true if a pivot was not positive and finite (wave-uniform; tested on the
+// high word in scalar ALU: pivots below 2^-1022 count as not positive).
+__device__ __forceinline__ bool panel(double* DTk, const double* UN, int lane) {
   const int i = lane & 15;
   const bool erow = (lane >= 16 && lane < 32);
+  const double* src = erow ? UN + unit_row(i) : DTk + i * 16;
   double v[16];
 #pragma unroll
   for (int c = 0; c < 16; c += 2) {
-    const double2 a2 = *(const double2*)(DTk + i * 16 + c);
+    const double2 a2 = *(const double2*)(src + c);
     v[c] = a2.x;
     v[c + 1] = a2.y;
   }
-  // materialise the loads in every lane before the select (otherwise the loads are
-  // sunk into 16 exec-masked branches)
-#pragma unroll
-  for (int c = 0; c < 16; ++c) asm volatile("" : "+v"(v[c]));
-#pragma unroll
-  for (int c = 0; c < 16; ++c) v[c] = erow ? (c == i ? 1.0 : 0.0) : -v[c];  // DT holds -A_kk
-  bool bad = false;
+  unsigned bad = 0;
 #pragma unroll
   for (int c = 0; c < 16; ++c) {
     const double piv = readlane_d(v[c], c);
-    bad |= !(piv > 0.0 && piv < INFINITY);
-    const double q = v[c] * rsqrt_pivot(piv);
+    bad |= (unsigned)__double2hiint(piv) - 1u >= 0x7FEFFFFFu;  // not in [2^-1022, inf)
+    double q = v[c] * rsqrt_pivot(piv);
     v[c] = q;
     if (c < 15) {
       // L column c (the row lanes' q) into both 16-lane rows, then for j > c
       // v[j] -= L_jc q with L_jc broadcast from lane j of the row by the fma itself
       double lq = row0_both(q);
-      const double nq = -q;
 #pragma unroll
-      for (int j = c + 1; j < 16; ++j) fmac_rowbcast(v[j], lq, nq, j, j == c + 1);
+      for (int j = c + 1; j < 16; ++j) fnmac_rowbcast(v[j], lq, q, j, j == c + 1);
     }
   }
   if (erow) {
 #pragma unroll
     for (int j = 0; j < 16; ++j) DTk[i * LIS + j] = v[j];  // (L^-T)[t][j] = (L^-1)[j][t]
   }
-  return bad;
+  return bad != 0;
 }
 
 // y = L^-1 b for one block (L^-T stored with row stride LIS), by a whole wave:
@@ -1164,12 +1176,12 @@ __device__ __forceinline__ bool factor_forward(const GnArgs& a, const SmemLayout
           v[r] = PB[r * 64 + lane_o];
         }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) t = __builtin_amdgcn_mfma_f64_16x16x4f64(v[r], v[r], t, 0, 0, 0);
+        for (int r = 0; r < 4; ++r) t = __builtin_amdgcn_mfma_f64_16x16x4f64(v[r], v[r], t, 0, 0, MFMA_NEG_A);
 #pragma unroll
         for (int r = 0; r < 4; ++r) DTn[r * 64 + lane_o] = t[r];
         wave_lds_sync();
       }
-      if (!KO(3)) bad |= panel(DTn, lane_o);
+      if (!KO(3)) bad |= panel(DTn, sm + SL.UN, lane_o);
       __builtin_amdgcn_s_setprio(0);
     } else if (k >= 0 && !KO(4)) {
       // b_b -= U_kb^T y_k for b >= k + 1: one output per lane of the other waves
@@ -1219,7 +1231,7 @@ __device__ __forceinline__ bool factor_forward(const GnArgs& a, const SmemLayout
         v[r] = PB[(J - k - 1) * 256 + r * 64 + lane_o];
       }
 #pragma unroll
-      for (int r = 0; r < 4; ++r) t = __builtin_amdgcn_mfma_f64_16x16x4f64(v[r], v[r], t, 0, 0, 0);
+      for (int r = 0; r < 4; ++r) t = __builtin_amdgcn_mfma_f64_16x16x4f64(v[r], v[r], t, 0, 0, MFMA_NEG_A);
 #pragma unroll
       for (int r = 0; r < 4; ++r) DTj[r * 64 + lane_o] = t[r];
     }
@@ -1387,6 +1399,7 @@ __global__ __launch_bounds__(NTHREADS, NW / 2) void k_gn(GnArgs a) {  // 2nd arg
   init_rowmask((int*)(sm + SL.ROWM), wave, lane, stab);
   double* Xs = sm + SL.Xs;
   if (threadIdx.x == 0) *(int*)(sm + SL.RED + 4 * NW) = 0;  // NOT_SPD flag
+  init_units(sm + SL.UN);
   double* DV = sm + SL.YV;  // delta after backward()
   double* RED = sm + SL.RED;
   d4 acc[SLOTS];
@@ -1455,7 +1468,7 @@ __global__ __launch_bounds__(NTHREADS, NW / 2) void k_gn(GnArgs a) {  // 2nd arg
       __syncthreads();  // diagonal tiles (LDS) complete
       for (int t = threadIdx.x; t < a.NT * 256; t += NTHREADS) {
         const int J = t >> 8, tr = (t >> 4) & 15, tc = t & 15;
-        Hb[(size_t)(16 * J + tr) * dp + 16 * J + tc] = -sm[SL.DT + J * DTS + (t & 255)];
+        Hb[(size_t)(16 * J + tr) * dp + 16 * J + tc] = sm[SL.DT + J * DTS + (t & 255)];
       }
       for (int t = threadIdx.x; t < dp; t += NTHREADS) a.gout[(size_t)b * dp + t] = -sm[SL.BV + t];
       if (threadIdx.x == 0) a.cost[b] = c1;
@@ -1588,6 +1601,7 @@ __global__ __launch_bounds__(NTHREADS, NW / 2) void k_gn_bounded(GnArgs a) {
   const double* DV = sm + SL.YV;  // step after backward()
   double* RED = sm + SL.RED;
   if (threadIdx.x == 0) *(int*)(sm + SL.RED + 4 * NW) = 0;  // NOT_SPD flag
+  init_units(sm + SL.UN);
   d4 acc[SLOTS];
 #pragma unroll
   for (int s = 0; s < SLOTS; ++s) acc[s] = d4{0.0, 0.0, 0.0, 0.0};

@@ -1,5 +1,6 @@
 // Dependent-latency microbenchmarks of the primitives the panel is built from
-// (tools only): one wave, a chain of 64 dependent ops, cycles per op.
+// (tools only): one wave, a chain of 64 dependent ops, cycles per op; 9..13 are
+// throughput (8 independent chains).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 typedef double d4 __attribute__((ext_vector_type(4)));
@@ -12,11 +13,16 @@ __device__ __forceinline__ double rl(double v, int lane) {
 }
 
 template <int which>
-__global__ __launch_bounds__(64) void k_lat(double* out, unsigned long long* cyc) {
-  const int lane = threadIdx.x;
+__global__ __launch_bounds__(1024) void k_lat(double* out, unsigned long long* cyc) {
+  const int lane = threadIdx.x & 63;
   double x = 1.0 + lane * 1e-3, y = 0.999;
   asm volatile("" : "+v"(x), "+v"(y));
   d4 c = {x, x, x, x};
+  double z[8];
+  int w[8], sreg[8];
+  unsigned long long sm64[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { z[k] = x + k; w[k] = lane + k; sreg[k] = k; sm64[k] = 0; asm volatile("" : "+v"(z[k]), "+v"(w[k]), "+s"(sreg[k])); }
   const unsigned long long t0 = __builtin_amdgcn_s_memtime();
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -34,20 +40,50 @@ __global__ __launch_bounds__(64) void k_lat(double* out, unsigned long long* cyc
     } else if constexpr (which == 6) x = x * y;                                      // f64 mul chain
     else if constexpr (which == 7) { x = __builtin_amdgcn_rcp(x) + 0.5; }           // rcp f64
     else if constexpr (which == 8) { c = __builtin_amdgcn_mfma_f64_16x16x4f64(x, y, c, 0, 0, 0); x = c[1] * y; }  // MFMA -> VALU -> MFMA
+    else if constexpr (which == 9) { z[i & 7] = fma(z[i & 7], y, 1e-9); }          // 8 independent fma chains
+    else if constexpr (which == 10) {                                               // 8 independent DPP64 fmac chains
+      asm("v_fmac_f64_dpp %0, %1, %2 row_newbcast:3 row_mask:0xf bank_mask:0xf" : "+v"(z[i & 7]) : "v"(x), "v"(y));
+    } else if constexpr (which == 11) {                                             // 8 independent non-DPP fmac (asm)
+      asm("v_fmac_f64 %0, %1, %2" : "+v"(z[i & 7]) : "v"(x), "v"(y));
+    } else if constexpr (which == 12) {                                             // DPP64 fmac, row_mask 0x1
+      asm("v_fmac_f64_dpp %0, %1, %2 row_newbcast:3 row_mask:0x1 bank_mask:0xf" : "+v"(z[i & 7]) : "v"(x), "v"(y));
+    } else if constexpr (which == 13) {                                             // 8 independent mul
+      z[i & 7] = z[i & 7] * y;
+    } else if constexpr (which == 14) {                                             // v_mov_b32
+      asm volatile("v_mov_b32 %0, %1" : "=v"(w[i & 7]) : "v"(w[(i + 3) & 7]));
+    } else if constexpr (which == 15) {                                             // v_mov_b64
+      asm volatile("v_mov_b64 %0, %1" : "=v"(z[i & 7]) : "v"(z[(i + 3) & 7]));
+    } else if constexpr (which == 16) {                                             // v_permlane16_swap
+      asm volatile("v_permlane16_swap_b32 %0, %1" : "+v"(w[i & 7]), "+v"(w[(i + 4) & 7]));
+    } else if constexpr (which == 17) {                                             // v_readlane
+      asm volatile("v_readlane_b32 %0, %1, 5" : "=s"(sreg[i & 7]) : "v"(w[i & 7]));
+    } else if constexpr (which == 18) {                                             // v_cmp_class_f64
+      asm volatile("v_cmp_class_f64 %0, %1, %2" : "=s"(sm64[i & 7]) : "v"(z[i & 7]), "v"(w[0]));
+    } else if constexpr (which == 19) {                                             // v_add_u32
+      asm volatile("v_add_u32 %0, %1, %2" : "=v"(w[i & 7]) : "v"(w[(i + 3) & 7]), "v"(w[(i + 5) & 7]));
+    } else if constexpr (which == 20) {                                             // s_add_u32
+      asm volatile("s_add_u32 %0, %1, 7" : "=s"(sreg[i & 7]) : "s"(sreg[(i + 3) & 7]) : "scc");
+    } else if constexpr (which == 21) {                                             // v_rsq_f64 independent
+      z[i & 7] = __builtin_amdgcn_rsq(z[(i + 3) & 7]);
+    } else if constexpr (which == 22) {                                             // v_mov_b32_dpp quad_perm
+      w[i & 7] = __builtin_amdgcn_mov_dpp(w[(i + 3) & 7], 0xB1, 0xF, 0xF, false);
+    }
   }
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   asm volatile("" ::"v"(x), "v"(c));
+#pragma unroll
+  for (int k = 0; k < 8; ++k) asm volatile("" ::"v"(z[k]), "v"(w[k]), "s"(sreg[k]), "s"(sm64[k]));
   __builtin_amdgcn_sched_barrier(0);
   const unsigned long long t1 = __builtin_amdgcn_s_memtime();
-  out[lane] = x + c[0] + c[1] + c[2] + c[3];
-  if (lane == 0) *cyc = t1 - t0;
+  out[threadIdx.x] = x + c[0] + c[1] + c[2] + c[3];
+  if (lane == 0) cyc[threadIdx.x >> 6] = t1 - t0;
 }
 
-extern "C" int lat_run(int which, double* out, unsigned long long* cyc) {
+extern "C" int lat_run(int which, double* out, unsigned long long* cyc, int nthreads) {
   switch (which) {
-#define L(w) case w: hipLaunchKernelGGL(k_lat<w>, dim3(1), dim3(64), 0, 0, out, cyc); break;
-    L(0) L(1) L(2) L(3) L(4) L(5) L(6) L(7) L(8)
+#define L(w) case w: hipLaunchKernelGGL(k_lat<w>, dim3(1), dim3(nthreads), 0, 0, out, cyc); break;
+    L(0) L(1) L(2) L(3) L(4) L(5) L(6) L(7) L(8) L(9) L(10) L(11) L(12) L(13) L(14) L(15) L(16) L(17) L(18) L(19) L(20) L(21) L(22)
 #undef L
   }
   return (int)hipDeviceSynchronize();
