@@ -1027,17 +1027,22 @@ __device__ __forceinline__ void fnmac_rowbcast(double& acc, double& src0, double
 #undef MHE_FMAC_BCAST
 
 // The value of the first 16-lane row (lanes 0..15) in the first two rows: element
-// [0] of v_permlane16_swap with the same register as both operands.
+// [0] of v_permlane16_swap over two copies of v (two 64-bit moves instead of four
+// 32-bit ones: the copies are opaque, so the swaps consume them in place).
 __device__ __forceinline__ double row0_both(double v) {
-  const long long b = __double_as_longlong(v);
-  const auto l = __builtin_amdgcn_permlane16_swap((int)b, (int)b, false, false);
-  const auto h = __builtin_amdgcn_permlane16_swap((int)(b >> 32), (int)(b >> 32), false, false);
+  double t1 = v, t2 = v;
+  asm volatile("" : "+v"(t1), "+v"(t2));
+  const long long b1 = __double_as_longlong(t1), b2 = __double_as_longlong(t2);
+  const auto l = __builtin_amdgcn_permlane16_swap((int)b1, (int)b2, false, false);
+  const auto h = __builtin_amdgcn_permlane16_swap((int)(b1 >> 32), (int)(b2 >> 32), false, false);
   return __longlong_as_double(((long long)h[0] << 32) | (unsigned int)l[0]);
 }
 
 // 1/sqrt(x) for a positive finite pivot: hardware v_rsq_f64 (~1e-9 relative)
 // refined by one Newton step (error squared: ~1 ulp).  Non-positive or
 // non-finite pivots are flagged by the caller and poison the factor anyway.
+// (Writing the step as four instructions with the halving in the fma's output
+// modifier needs inline asm, and then a wait state of its own after the rsq: no gain.)
 __device__ __forceinline__ double rsqrt_pivot(double x) {
   const double r = __builtin_amdgcn_rsq(x);
   const double e = fma(-x * r, r, 1.0);  // 1 - x r^2

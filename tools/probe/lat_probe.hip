@@ -67,6 +67,12 @@ __global__ __launch_bounds__(1024) void k_lat(double* out, unsigned long long* c
       z[i & 7] = __builtin_amdgcn_rsq(z[(i + 3) & 7]);
     } else if constexpr (which == 22) {                                             // v_mov_b32_dpp quad_perm
       w[i & 7] = __builtin_amdgcn_mov_dpp(w[(i + 3) & 7], 0xB1, 0xF, 0xF, false);
+    } else if constexpr (which == 23) {                                             // s_nop 0
+      asm volatile("s_nop 0");
+    } else if constexpr (which == 24) {                                             // s_nop 1
+      asm volatile("s_nop 1");
+    } else if constexpr (which == 25) {                                             // v_mov_b32 + s_nop 1 pairs
+      asm volatile("v_mov_b32 %0, %1\n\ts_nop 1" : "=v"(w[i & 7]) : "v"(w[(i + 3) & 7]));
     }
   }
   __builtin_amdgcn_sched_barrier(0);
@@ -83,7 +89,7 @@ __global__ __launch_bounds__(1024) void k_lat(double* out, unsigned long long* c
 extern "C" int lat_run(int which, double* out, unsigned long long* cyc, int nthreads) {
   switch (which) {
 #define L(w) case w: hipLaunchKernelGGL(k_lat<w>, dim3(1), dim3(nthreads), 0, 0, out, cyc); break;
-    L(0) L(1) L(2) L(3) L(4) L(5) L(6) L(7) L(8) L(9) L(10) L(11) L(12) L(13) L(14) L(15) L(16) L(17) L(18) L(19) L(20) L(21) L(22)
+    L(0) L(1) L(2) L(3) L(4) L(5) L(6) L(7) L(8) L(9) L(10) L(11) L(12) L(13) L(14) L(15) L(16) L(17) L(18) L(19) L(20) L(21) L(22) L(23) L(24) L(25)
 #undef L
   }
   return (int)hipDeviceSynchronize();

@@ -6,7 +6,7 @@ names = ["v_fma_f64", "v_rsq_f64 + add", "2 v_readlane + mul", "MFMA f64 16x16x4
          "2 v_permlane16_swap + mul", "v_mul_f64", "v_rcp_f64 + add", "MFMA -> VALU mul -> MFMA",
          "tput v_fma_f64 (8 chains)", "tput v_fmac_f64_dpp newbcast", "tput v_fmac_f64 (asm)", "tput fmac_dpp row_mask 1", "tput v_mul_f64",
          "tput v_mov_b32", "tput v_mov_b64", "tput v_permlane16_swap", "tput v_readlane_b32", "tput v_cmp_class_f64",
-         "tput v_add_u32", "tput s_add_u32", "tput v_rsq_f64", "tput v_mov_b32_dpp"]
+         "tput v_add_u32", "tput s_add_u32", "tput v_rsq_f64", "tput v_mov_b32_dpp", "s_nop 0", "s_nop 1", "v_mov_b32 + s_nop 1"]
 print("waves per SIMD:                      1        2        4")
 for w, nm in enumerate(names):
     row = []
