@@ -569,7 +569,7 @@ __device__ __forceinline__ double meas_phase(const GnArgs& a, const ConstLayout&
 // 16 L2 loads in flight instead of 8, halving the dependent round trips.
 template <class DYN, class MEAS, bool HUBER = false>
 __device__ __forceinline__ double node_meas_phase(const GnArgs& a, const ConstLayout& CL, const SmemLayout& SL,
-                                                  double* sm, int b) {
+                                                  double* sm, int b, DIAG_FDECL) {
   constexpr int n = DYN::n;
   constexpr int ROWS = NTHREADS / TPR;
   if (a.P > ROWS || a.M > ROWS)
@@ -626,12 +626,20 @@ __device__ __forceinline__ double node_meas_phase(const GnArgs& a, const ConstLa
     dx[c] += dpp_d<0x4E>(dx[c]);
     xi[c] += dpp_d<0x4E>(xi[c]);
   }
+  DIAG_MARK(14);
   double cost = 0.0;
   if (part == 0) {
     if (r < a.P) cost += node_row<DYN, HUBER>(a, CL, SL, sm, b, r, dx);
     if (r < a.M) cost += meas_row<DYN, MEAS>(a, CL, SL, sm, b, r, xi);
   }
   return cost;
+}
+
+template <class DYN, class MEAS, bool HUBER = false>
+__device__ __forceinline__ double node_meas_phase(const GnArgs& a, const ConstLayout& CL, const SmemLayout& SL,
+                                                  double* sm, int b) {
+  DIAG_DECL
+  return node_meas_phase<DYN, MEAS, HUBER>(a, CL, SL, sm, b, DIAG_FARGS);
 }
 
 // Gradient g = J^T W r (nlp/nlp.py:242-286 objective); writes BV = -g (padding 0).
@@ -1438,9 +1446,8 @@ __global__ __launch_bounds__(NTHREADS, NW / 2) void k_gn(GnArgs a) {  // 2nd arg
   DIAG_DECL
   for (;;) {
     DIAG_MARK(7);
-    double c1 = node_meas_phase<DYN, MEAS, HUBER>(FA, FCL, FSL, sm, opaque_s(b));
+    double c1 = node_meas_phase<DYN, MEAS, HUBER>(FA, FCL, FSL, sm, opaque_s(b), DIAG_FARGS);
     DIAG_MARK(6);
-    DIAG_MARK(14);
     __syncthreads();
     DIAG_MARK(0);
     c1 += grad_phase<DYN>(FA, FCL, FSL, sm, opaque_s(b));

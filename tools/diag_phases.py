@@ -33,7 +33,7 @@ X, c, it, st = s.solve(w.X_init, w.U, w.Y, max_iter=iters, tol=0.0)
 ev1.record()
 torch.cuda.synchronize()
 d = dbg.view(B, 16).cpu().numpy().astype(np.float64) / iters
-names = {7: "loop head", 6: "node", 14: "meas", 0: "node+meas barrier", 1: "gradient", 15: "tile build", 2: "tile barrier", 3: "chol tail", 4: "backward", 5: "exit",
+names = {7: "loop head", 6: "node/meas rows", 14: "node mat-vec loop", 0: "node+meas barrier", 1: "gradient", 15: "tile build", 2: "tile barrier", 3: "chol tail", 4: "backward", 5: "exit",
          8: "  T (trsm)", 9: "  barrier1", 12: "  U: rhs/panel", 13: "  U: slots", 10: "  U: diag", 11: "  barrier2"}
 tot = d.sum(1).mean()
 print(f"B={B} iters={iters} kernel {ev0.elapsed_time(ev1):.3f} ms; cycles/iter/WG (s_memtime) total {tot:.0f}")

@@ -94,3 +94,21 @@ extern "C" int lat_run(int which, double* out, unsigned long long* cyc, int nthr
   }
   return (int)hipDeviceSynchronize();
 }
+
+// Dependent-load latency (pointer chase over `n` ints with stride `st`), one wave:
+// cycles per load; n * 4 B > 32 KB misses the L1, < 4 MB hits the L2.
+__global__ __launch_bounds__(64) void k_chase(const int* buf, int steps, int* out, unsigned long long* cyc) {
+  int idx = threadIdx.x;
+  for (int w = 0; w < 64; ++w) idx = buf[idx];  // warm
+  __builtin_amdgcn_s_waitcnt(0);
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  for (int i = 0; i < steps; ++i) idx = buf[idx];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+  out[threadIdx.x] = idx;
+  if (threadIdx.x == 0) *cyc = (t1 - t0) / steps;
+}
+extern "C" int chase_run(const int* buf, int steps, int* out, unsigned long long* cyc) {
+  hipLaunchKernelGGL(k_chase, dim3(1), dim3(64), 0, 0, buf, steps, out, cyc);
+  return (int)hipDeviceSynchronize();
+}

@@ -15,3 +15,11 @@ for w, nm in enumerate(names):
             lib.lat_run(w, ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(cyc.data_ptr()), nt)
         row.append(cyc[: nt // 64].double().mean().item() / 64)
     print(f"{nm:32s} " + " ".join(f"{v:8.1f}" for v in row) + "  cycles/op per wave")
+# dependent global loads: lane l follows its own chain, stride 33 ints (distinct lines)
+for n in (2048, 1 << 16, 1 << 20, 1 << 26):
+    idx = (torch.arange(n, dtype=torch.int64) + 64 * 33) % n
+    buf = idx.to(torch.int32).cuda()
+    o = torch.zeros(64, dtype=torch.int32, device="cuda")
+    for _ in range(2):
+        lib.chase_run(ctypes.c_void_p(buf.data_ptr()), 256, ctypes.c_void_p(o.data_ptr()), ctypes.c_void_p(cyc.data_ptr()))
+    print(f"pointer chase over {n * 4 / 1024:9.0f} KB: {cyc[0].item():6d} cycles per dependent load")
