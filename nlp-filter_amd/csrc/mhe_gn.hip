@@ -564,6 +564,23 @@ __device__ __forceinline__ double meas_phase(const GnArgs& a, const ConstLayout&
   return cost;
 }
 
+// v plus the value of the paired 16-lane row (rows 0+1, 2+3), in every lane
+// (v_permlane16_swap; the sum is formed in the same order on both rows).
+__device__ __forceinline__ double row_pair_sum(double v) {
+  const long long b = __double_as_longlong(v);
+  const auto l = __builtin_amdgcn_permlane16_swap((int)b, (int)b, false, false);
+  const auto h = __builtin_amdgcn_permlane16_swap((int)(b >> 32), (int)(b >> 32), false, false);
+  return __longlong_as_double(((long long)h[0] << 32) | (unsigned int)l[0]) +
+         __longlong_as_double(((long long)h[1] << 32) | (unsigned int)l[1]);
+}
+// In lanes 0..31: the value of lane + 32 (v_permlane32_swap).
+__device__ __forceinline__ double upper_half(double v) {
+  const long long b = __double_as_longlong(v);
+  const auto l = __builtin_amdgcn_permlane32_swap((int)b, (int)b, false, false);
+  const auto h = __builtin_amdgcn_permlane32_swap((int)(b >> 32), (int)(b >> 32), false, false);
+  return __longlong_as_double(((long long)h[1] << 32) | (unsigned int)l[1]);
+}
+
 // node_phase + meas_phase.  When both row counts fit one pass (P, M <= 128 with
 // 4 lanes per row: C1, C2) each lane runs its D-row and Phi-row dots together,
 // 16 L2 loads in flight instead of 8, halving the dependent round trips.
@@ -576,8 +593,11 @@ __device__ __forceinline__ double node_meas_phase(const GnArgs& a, const ConstLa
     return node_phase<DYN, HUBER>(a, CL, SL, sm, b) + meas_phase<DYN, MEAS>(a, CL, SL, sm, b);
   const __amdgpu_buffer_rsrc_t rs = cbuf_rsrc(a.cbuf, CL.total);
   const double* Xs = sm + SL.Xs;
+  // the TPR = 4 parts of a row are the four 16-lane rows of a wave (row = 16 wave +
+  // lane % 16): the 4 lanes of a quad read 4 consecutive rows of D^T / Phi^T, one
+  // 32-B piece of one line (with the parts in a quad they touched 4 lines)
   const int tid = opaque_tid();
-  const int part = tid % TPR, r = tid / TPR;
+  const int part = (tid >> 4) & 3, r = (tid >> 6) * 16 + (tid & 15);
   const int kk = r < a.P ? r : a.P - 1, ii = r < a.M ? r : a.M - 1;
   double dx[n], xi[n];
 #pragma unroll
@@ -616,15 +636,16 @@ __device__ __forceinline__ double node_meas_phase(const GnArgs& a, const ConstLa
       xi[c] += m2 * Xs[j * n + c];
     }
   }
+  static_assert(TPR == 4, "the row reductions below assume 4 parts per row");
 #pragma unroll
   for (int c = 0; c < n; ++c) {
-    dx[c] += dpp_d<0xB1>(dx[c]);
-    xi[c] += dpp_d<0xB1>(xi[c]);
+    dx[c] = row_pair_sum(dx[c]);  // (part 0 + part 1), (part 2 + part 3)
+    xi[c] = row_pair_sum(xi[c]);
   }
 #pragma unroll
   for (int c = 0; c < n; ++c) {
-    dx[c] += dpp_d<0x4E>(dx[c]);
-    xi[c] += dpp_d<0x4E>(xi[c]);
+    dx[c] += upper_half(dx[c]);  // complete in lanes 0..15 (part 0)
+    xi[c] += upper_half(xi[c]);
   }
   DIAG_MARK(14);
   double cost = 0.0;
@@ -660,11 +681,13 @@ __device__ __forceinline__ double grad_phase(const GnArgs& a, const ConstLayout&
   const int tid = opaque_tid();
   // TPR lanes per node: the first half sums the D column (sum_k D[k][j] V_k), the
   // second half the Phi column (sum_i Phi[i][j] GE_i), each split over TPR/2 lanes
+  // (the TPR lanes of a node are the four 16-lane rows of a wave, node = 16 wave +
+  // lane % 16: a quad reads 4 consecutive columns of D / Phi, as in node_meas_phase)
   constexpr int HP = TPR / 2;
-  const int q = tid % TPR, sub = q % HP;
+  const int q = (tid >> 4) & 3, sub = q % HP;
   const bool phi = q >= HP;
   for (int j0 = 0; j0 < a.P; j0 += NTHREADS / TPR) {
-    const int j = j0 + tid / TPR;
+    const int j = j0 + (tid >> 6) * 16 + (tid & 15);
     const int jj = j < a.P ? j : a.P - 1;
     const double* vec = phi ? GE : Vs;
     const int len = phi ? a.M : a.P;
@@ -692,12 +715,12 @@ __device__ __forceinline__ double grad_phase(const GnArgs& a, const ConstLayout&
 #pragma unroll
       for (int c = 0; c < n; ++c) s[c] += mv * vec[k * n + c];
     }
-    static_assert(HP == 2, "quad DPP reductions below assume TPR == 4");
+    static_assert(HP == 2, "the row reductions below assume TPR == 4");
 #pragma unroll
-    for (int c = 0; c < n; ++c) s[c] += dpp_d<0xB1>(s[c]);  // lane ^ 1
+    for (int c = 0; c < n; ++c) s[c] = row_pair_sum(s[c]);  // rows 0+1: D column, rows 2+3: Phi column
     double o[n];
 #pragma unroll
-    for (int c = 0; c < n; ++c) o[c] = dpp_d<0x4E>(s[c]);  // lane ^ 2: the other column's sum
+    for (int c = 0; c < n; ++c) o[c] = upper_half(s[c]);  // in row 0: the Phi column's sum
     if (q != 0 || j >= a.P) continue;
     double gv[n];
 #pragma unroll
