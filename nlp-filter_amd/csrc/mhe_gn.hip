@@ -812,12 +812,16 @@ __device__ __forceinline__ void build_slots_n2(const GnArgs& a, const ConstLayou
     double dav[4], dbv[4];
     spread_dblock(av, dav);
     spread_dblock(bv, dbv);
+    // the row's component aa = row & 1 is the same for the four registers (rows
+    // differ by 4), so E_l[aa][bb] is one LDS read per slot; padding rows (row >= d)
+    // read a clamped node and are replaced by -Cc below
+    const int aa = (lane >> 4) & 1;
+    const double el = Es[(l * 2 + aa) * 2 + bb];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int row = 16 * J + (lane >> 4) + 4 * r;
-      const int rr = row < a.d ? row : a.d - 1;
-      const int j = rr >> 1, aa = rr & 1;
-      const double t = dav[r] * Es[(l * 2 + aa) * 2 + bb] + dbv[r] * Es[(j * 2 + bb) * 2 + aa];
+      const int j = min(row >> 1, a.P - 1);
+      const double t = dav[r] * el + dbv[r] * Es[(j * 2 + bb) * 2 + aa];
       acc[s][r] = (row < a.d && col < a.d) ? t - c[r] : -c[r];
       if (BOUNDED && (ACT[row] | ACT[col])) acc[s][r] = 0.0;
     }
