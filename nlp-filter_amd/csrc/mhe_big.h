@@ -630,7 +630,7 @@ __global__ __launch_bounds__(BIG_NTHREADS, BIG_JB == 8 ? 2 : 4) void k_big_chol(
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const double v = Lt[64 * r + lane];
-            c = __builtin_amdgcn_mfma_f64_16x16x4f64(-v, v, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f64_16x16x4f64(v, v, c, 0, 0, MFMA_NEG_A);
           }
         }
 #pragma unroll
@@ -653,7 +653,7 @@ __global__ __launch_bounds__(BIG_NTHREADS, BIG_JB == 8 ? 2 : 4) void k_big_chol(
             const double* LI = H + (size_t)big_tile_index(I, k0 + kk, NT) * 256;
 #pragma unroll
             for (int r = 0; r < 4; ++r)
-              c = __builtin_amdgcn_mfma_f64_16x16x4f64(-Lk[64 * r + lane], LI[64 * r + lane], c, 0, 0, 0);
+              c = __builtin_amdgcn_mfma_f64_16x16x4f64(Lk[64 * r + lane], LI[64 * r + lane], c, 0, 0, MFMA_NEG_A);
           }
 #pragma unroll
           for (int r = 0; r < 4; ++r) Ak[64 * r + lane] = c[r];
@@ -717,20 +717,20 @@ __global__ __launch_bounds__(BIG_NTHREADS, BIG_JB == 8 ? 2 : 4) void k_big_chol(
         const double* LI0 = H + (size_t)big_tile_index(I, k0, NT) * 256;
         double av[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) av[r] = -LI0[64 * r + lane];
+        for (int r = 0; r < 4; ++r) av[r] = LI0[64 * r + lane];  // negated by the MFMA (MFMA_NEG_A)
 #pragma unroll 1
         for (int kk = 0; kk < kb; ++kk) {
           double an[4];
           const double* LIn = H + (size_t)big_tile_index(I, k0 + min(kk + 1, kb - 1), NT) * 256;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) an[r] = -LIn[64 * r + lane];
+          for (int r = 0; r < 4; ++r) an[r] = LIn[64 * r + lane];
 #pragma unroll
           for (int jj = 0; jj < BIG_JB; ++jj) {
             if (jj < jmax) {
               const double* Bt = LJ + (jj * kb + kk) * 256;
 #pragma unroll
               for (int r = 0; r < 4; ++r)
-                c[jj] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[r], Bt[64 * r + lane], c[jj], 0, 0, 0);
+                c[jj] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[r], Bt[64 * r + lane], c[jj], 0, 0, MFMA_NEG_A);
             }
           }
 #pragma unroll
@@ -868,11 +868,11 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_border(BigArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           c[r] = Zp[(size_t)ii * dp + 16 * I + mg + 4 * r];
-          av[r] = -L[(4 * r + mg) * 16 + ii];  // L_Ik[i][m], k-major tile
+          av[r] = L[(4 * r + mg) * 16 + ii];  // L_Ik[i][m], k-major tile (negated by the MFMA)
           bv[r] = zload(k, r);
         }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) c = __builtin_amdgcn_mfma_f64_16x16x4f64(av[r], bv[r], c, 0, 0, 0);
+        for (int r = 0; r < 4; ++r) c = __builtin_amdgcn_mfma_f64_16x16x4f64(av[r], bv[r], c, 0, 0, MFMA_NEG_A);
 #pragma unroll
         for (int r = 0; r < 4; ++r) Zp[(size_t)ii * dp + 16 * I + mg + 4 * r] = c[r];
       }
@@ -900,11 +900,11 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_border(BigArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           c[r] = Zp[(size_t)ii * dp + 16 * J + mg + 4 * r];
-          av[r] = -L[ii * 16 + 4 * r + mg];  // (L_kJ^T)[i][m] = L_kJ[m][i], k-major tile
+          av[r] = L[ii * 16 + 4 * r + mg];  // (L_kJ^T)[i][m] = L_kJ[m][i], k-major tile (negated by the MFMA)
           bv[r] = zload(k, r);
         }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) c = __builtin_amdgcn_mfma_f64_16x16x4f64(av[r], bv[r], c, 0, 0, 0);
+        for (int r = 0; r < 4; ++r) c = __builtin_amdgcn_mfma_f64_16x16x4f64(av[r], bv[r], c, 0, 0, MFMA_NEG_A);
 #pragma unroll
         for (int r = 0; r < 4; ++r) Zp[(size_t)ii * dp + 16 * J + mg + 4 * r] = c[r];
       }

@@ -1183,13 +1183,13 @@ __device__ __forceinline__ bool factor_forward(const GnArgs& a, const SmemLayout
       const double* LT = DT + k * DTS;
       double la[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) la[r] = -LT[(4 * r + (lane_o >> 4)) * LIS + (lane_o & 15)];  // -L^-1[l&15][4r+(l>>4)]
+      for (int r = 0; r < 4; ++r) la[r] = LT[(4 * r + (lane_o >> 4)) * LIS + (lane_o & 15)];  // L^-1[l&15][4r+(l>>4)], negated by the MFMA
 #pragma unroll
       for (int s = 0; s < SLOTS; ++s) {
         if ((mT >> s) & 1u) {
           d4 u = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-          for (int r = 0; r < 4; ++r) u = __builtin_amdgcn_mfma_f64_16x16x4f64(la[r], acc[s][r], u, 0, 0, 0);
+          for (int r = 0; r < 4; ++r) u = __builtin_amdgcn_mfma_f64_16x16x4f64(la[r], acc[s][r], u, 0, 0, MFMA_NEG_A);
           if (!KO(0)) acc[s] = u;
           const int I = slot_ij(stab_o, s) & 0xffff;
 #pragma unroll
