@@ -822,7 +822,12 @@ __device__ __forceinline__ void build_slots_n2(const GnArgs& a, const ConstLayou
       const int row = 16 * J + (lane >> 4) + 4 * r;
       const int j = min(row >> 1, a.P - 1);
       const double t = dav[r] * el + dbv[r] * Es[(j * 2 + bb) * 2 + aa];
-      acc[s][r] = (row < a.d && col < a.d) ? t - c[r] : -c[r];
+      // padding lies only in the last tile column (off-diagonal tiles have no padding
+      // rows): a wave-uniform test, the per-element select only there
+      if (I == a.NT - 1)
+        acc[s][r] = (row < a.d && col < a.d) ? t - c[r] : -c[r];
+      else
+        acc[s][r] = t - c[r];
       if (BOUNDED && (ACT[row] | ACT[col])) acc[s][r] = 0.0;
     }
     __builtin_amdgcn_sched_barrier(0);
