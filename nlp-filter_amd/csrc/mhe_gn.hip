@@ -817,13 +817,16 @@ __device__ __forceinline__ void build_slots_n2(const GnArgs& a, const ConstLayou
     // read a clamped node and are replaced by -Cc below
     const int aa = (lane >> 4) & 1;
     const double el = Es[(l * 2 + aa) * 2 + bb];
+    // off-diagonal tiles have no padding rows (16 J + 15 < 16 (NT - 1) < d): register
+    // r's row 16 J + (lane >> 4) + 4 r is node 8 J + (lane >> 5) + 2 r, so the four
+    // E_j[bb][aa] reads are one base address plus immediate offsets (8 doubles apart)
+    const double* ej = Es + ((8 * J + (lane >> 5)) * 2 + bb) * 2 + aa;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int row = 16 * J + (lane >> 4) + 4 * r;
-      const int j = min(row >> 1, a.P - 1);
-      const double t = dav[r] * el + dbv[r] * Es[(j * 2 + bb) * 2 + aa];
-      // padding lies only in the last tile column (off-diagonal tiles have no padding
-      // rows): a wave-uniform test, the per-element select only there
+      const double t = dav[r] * el + dbv[r] * ej[8 * r];
+      // padding lies only in the last tile column: a wave-uniform test, the
+      // per-element select only there
       if (I == a.NT - 1)
         acc[s][r] = (row < a.d && col < a.d) ? t - c[r] : -c[r];
       else
