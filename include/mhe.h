@@ -67,11 +67,14 @@ extern "C" {
 #define MHE_DYN_MULTI_RECEIVER 7         /* :81-96  n=8  m=0 */
 #define MHE_DYN_GNSS_TWO_RECEIVER 8      /* :98-115 n=10 m=6 */
 #define MHE_DYN_KINEMATIC_BICYCLE 9      /* :117-136 n=6 m=2 (kinematic_bycicle_and_bias) */
+#define MHE_DYN_VEHICLE_GNSS 10          /* :148-174 n=9 m=2 (vehicle_dynamics_and_gnss);
+                                            dyn_par = params["car_params"] as
+                                            [C_AF, C_AR, M, D_F, D_R, I_Z] */
 
 /* measurement plug-ins (reference nlp/measurements.py) */
 #define MHE_MEAS_FULL_STATE 1            /* :4-5   p=n, linear            */
 #define MHE_MEAS_PSEUDORANGE 2           /* :56-70 p=1, q=3 (sat_pos), idx[4] */
-#define MHE_MEAS_VEHICLE_PSEUDORANGE 3   /* :81-88 p=1, q=3               */
+#define MHE_MEAS_VEHICLE_PSEUDORANGE 3   /* :81-88 p=1, q=3 (x[0], x[1], x[8]; bias x[6]) */
 #define MHE_MEAS_RANGE_3D 4              /* :39-54 p=1, q=3 ("y" form), idx[3] */
 #define MHE_MEAS_MIXED 5                 /* several scalar plug-ins in one problem (one
                                             addResidualCost call each, nlp/nlp.py:258-277):
@@ -101,7 +104,15 @@ extern "C" {
 #define MHE_MAX_EXTRA 4   /* extra decision variables per trajectory */
 #define MHE_MAX_EQ 48     /* n_extra + n_eq */
 
+/* Every dims struct starts with struct_size: the caller sets it to sizeof() of
+ * the struct it declares, and every entry point returns MHE_ERR_DIMS (0 / -1 for
+ * the size queries) unless it equals this build's sizeof -- a binding that
+ * declares an older or truncated struct is refused before any later field is
+ * read.  (mhe/_lib.py sets it in the ctypes constructors.) */
+#define MHE_ABI_VERSION 3
+
 typedef struct mhe_dims {
+  int32_t struct_size;  /* = sizeof(mhe_dims)                                */
   int32_t N;            /* collocation order; P = N + 1 CGL nodes            */
   int32_t n;            /* state dimension   (must equal the model's)        */
   int32_t m;            /* control dimension (must equal the model's)        */
@@ -132,6 +143,8 @@ typedef struct mhe_dims {
                            dims alone; mhe_build_constants stamps it (with the
                            layout-defining dims) into the constants buffer and every
                            solve checks that stamp on the device.                 */
+  double dyn_par[8];    /* static dynamics parameters (model-defined, e.g.
+                           MHE_DYN_VEHICLE_GNSS); 0 for the parameter-free models   */
 } mhe_dims;
 
 /* Dynamics cost (addDynamicsCost, nlp/nlp.py:242-245): */
@@ -154,7 +167,8 @@ typedef struct mhe_dims {
  * not supported (MHE_ERR_UNSUPPORTED). */
 
 /* Size in bytes of the device constants buffer for `dims` (0 on bad dims).  The
- * last 256 bytes hold the layout stamp written by mhe_build_constants. */
+ * first 256 bytes are a header holding the layout stamp written by
+ * mhe_build_constants (offset 0: every solve checks it in bounds). */
 size_t mhe_const_bytes(const mhe_dims* dims);
 
 /*
@@ -240,6 +254,46 @@ int mhe_gn_solve_ext(const mhe_dims* dims, const void* const_buf, int32_t batch,
                      void* stream);
 
 /*
+ * All solve inputs and outputs in one struct (the entry point new bindings use;
+ * mhe_gn_solve / _ws / _ext are this call with Rw = NULL).  Pointers as
+ * mhe_gn_solve_ext, plus
+ *   Rw  (B|1, M, p, p)  per-solve measurement information, overriding the Rw the
+ *                       constants were built with (batch stride rw_bstride, 0 =
+ *                       shared; M scalars per trajectory for MHE_MEAS_MIXED).  The
+ *                       reference's MHE windows re-set R every window (R = 0 masks
+ *                       empty satellite slots, autonomous-car.py:250-263,
+ *                       gnss-multi-receiver.py:186-204): passing it here keeps one
+ *                       constants buffer for all windows.  Nonlinear measurement
+ *                       models only (a linear h has Rw folded into the constant
+ *                       part of J^T W J): MHE_ERR_UNSUPPORTED otherwise.
+ */
+typedef struct mhe_solve_args {
+  int32_t struct_size;     /* = sizeof(mhe_solve_args) */
+  int32_t batch;
+  const double* X0;
+  double* X_out;
+  const double* Z0;        /* extra variables (n_extra > 0), else NULL */
+  double* Z_out;
+  const double* U;
+  int64_t u_bstride;
+  const double* Y;
+  const double* PAR;
+  int64_t par_bstride;
+  const double* Rw;        /* optional, see above */
+  int64_t rw_bstride;
+  const double* x0;
+  double* cost_out;
+  int32_t* iters_out;
+  int32_t* status_out;
+  int32_t max_iter;
+  double tol;
+  void* workspace;         /* large-system path: >= mhe_workspace_bytes(dims, batch) */
+  size_t workspace_bytes;
+} mhe_solve_args;
+
+int mhe_solve(const mhe_dims* dims, const void* const_buf, const mhe_solve_args* args, void* stream);
+
+/*
  * Kernel-level parity: assemble the GN normal equations at X.
  *   H (B,dp,dp) full symmetric (dp = mhe_padded_dim; padding rows = identity),
  *   g (B,dp) gradient J^T W r (padding 0), cost (B).
@@ -270,6 +324,7 @@ int mhe_chol_solve(const mhe_dims* dims, const void* const_buf, int32_t batch,
 #define MHE_EKF_MEAS_MULTI_PSEUDORANGE_AND_BIAS 2 /* utils/gnss.py:48-61 (last row: bias, zero Jacobian row) */
 
 typedef struct mhe_ekf_dims {
+  int32_t struct_size; /* = sizeof(mhe_ekf_dims) */
   int32_t n, m;        /* state and control sizes of the dynamics model */
   int32_t pmax;        /* row capacity of Z / PAR / R per step (<= 32) */
   int32_t q;           /* parameters per measurement row (3) */
@@ -315,6 +370,7 @@ int mhe_ekf_run(const mhe_ekf_dims* dims, int32_t batch, int32_t steps, double* 
  * runLeastSquares (:97-141) for `chains` logs of `epochs` epochs each.
  * ------------------------------------------------------------------------ */
 typedef struct mhe_ls_dims {
+  int32_t struct_size; /* = sizeof(mhe_ls_dims) */
   int32_t slots;     /* satellite slots per epoch in the arrays (<= 64) */
   int32_t max_iter;  /* maxiter of iterativeLeastSquares (reference default 100); 0 = no position
                         iterations (velocity at x_init: iterativeLeastSquaresVel alone) */

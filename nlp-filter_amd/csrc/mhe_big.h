@@ -38,7 +38,7 @@ struct BigConst {  // byte offsets into the constants buffer
 
 __host__ __device__ inline BigConst big_const_layout(int P, int M, int n, int p, int nc = 0) {
   BigConst L;
-  size_t o = 0;
+  size_t o = CONST_HEADER;  // the layout stamp (mhe_core.h)
   const int Mr = M > 0 ? M : 1;
   L.D = o;     o = align256(o + sizeof(double) * P * P);
   L.Dt = o;    o = align256(o + sizeof(double) * P * P);
@@ -58,7 +58,7 @@ __host__ __device__ inline BigConst big_const_layout(int P, int M, int n, int p,
 }
 
 struct BigWs {  // per-trajectory workspace offsets in doubles
-  size_t H, LT, BV, YV, XE, GEe, Ge, Es, FtE, Vs, FtV, GZe, HZZe, GZVe, BM, ZM, DZ, ACT, total;
+  size_t H, LT, BV, YV, XE, GEe, Ge, Es, FtE, Vs, FtV, GZe, HZZe, GZVe, BM, ZM, DZ, ACT, GV, NZ, total;
 };
 
 // nz extra variables, nc equality constraints (border of the KKT system)
@@ -88,6 +88,9 @@ __host__ __device__ inline BigWs big_ws_layout(int P, int M, int n, int NT, int 
   W.ZM = o;   o = al(o + (size_t)((K + 15) / 16) * 16 * dp);     // H^-1 [H_xz C^T] (16-col panels)
   W.DZ = o;   o = al(o + (size_t)NZX);                           // z step
   W.ACT = o;  o = al(o + (size_t)dp / 2);                        // bounds: epsilon-active set (int per unknown)
+  W.GV = o;   o = al(o + (size_t)dp);                            // bounds: -g at the iterate (k_big_chol
+                                                                 // overwrites BV with the forward solve)
+  W.NZ = o;   o = al(o + 1);                                     // bounds: the cost's rounding level at X
   W.total = o;
   return W;
 }
@@ -115,14 +118,21 @@ struct BigArgs {
   double blb[8], bub[8];
   int nz, nc;        // extra variables / equality constraints (f4)
   double* Z;         // (B, nz) current extra variables (Z_out)
-  size_t tag_off;    // layout stamp of the constants buffer (mhe_build_constants)
-  unsigned long long tag;
+  unsigned long long tag;  // layout stamp expected at offset 0 of the constants buffer
   // component pairs (ca >= cb) of the measurement contraction, those whose G_e can be
   // nonzero first ("live": both components in the measurement Jacobian's support),
   // and the k_big_assemble chunking over them (BigPairPlan)
   int npr, nlive, nchl, pchl, nch;
   unsigned char pa[80], pb[80];
+  double dpar[8];    // mhe_dims.dyn_par (dynamics plug-in params)
+  const double* Rw;  // per-solve measurement weights (B|1, M, p, p) or NULL = the constants' Rw
+  long long rwstride;
 };
+
+// measurement weights of trajectory b: the per-solve array when given, else the constants'
+__device__ __forceinline__ const double* big_rw(const BigArgs& a, const double* Rc, int b) {
+  return a.Rw ? a.Rw + (long long)b * a.rwstride : Rc;
+}
 
 __device__ __forceinline__ int big_tile_index(int I, int J, int NT) { return J * NT - J * (J - 1) / 2 + (I - J); }
 
@@ -175,7 +185,7 @@ __device__ void big_active_set(const BigArgs& a, const double* X, const double* 
     if (lo > -INFINITY || hi < INFINITY) w = fmax(w, fabs(x - fmin(fmax(x - g, lo), hi)));
   }
   big_max2(red, w, xm);
-  const double eps = fmin(1e-6 * (1.0 + xm), w);  // EPS_ACT
+  const double eps = fmin(EPS_ACT * (1.0 + xm), w);
   for (int t = threadIdx.x; t < n * a.Pp; t += BIG_NTHREADS) {
     const int c = t / a.Pp, j = t % a.Pp;
     int act = 0;
@@ -204,7 +214,7 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_resid(BigArgs a, int final
   const double* cw = (const double*)(a.cbuf + CL.cw);
   const double* Qw = (const double*)(a.cbuf + CL.Qw);
   const double* Pw = (const double*)(a.cbuf + CL.Pw);
-  const double* Rw = (const double*)(a.cbuf + CL.Rw);
+  const double* Rw = big_rw(a, (const double*)(a.cbuf + CL.Rw), b);
   const double* PhiE = (const double*)(a.cbuf + CL.PhiE);
   const double* PhiET = (const double*)(a.cbuf + CL.PhiET);
   const int* erow = (const int*)(a.cbuf + CL.erow);
@@ -212,7 +222,7 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_resid(BigArgs a, int final
   const int Mr = a.M > 0 ? a.M : 1;
   const double* X = a.X + (size_t)b * a.P * n;
   __shared__ double red[2 * BIG_NW];
-  double cost = 0.0;
+  double cost = 0.0, noise = 0.0;  // noise: the cost's rounding level (bounded problems' line search)
   // interpolated states at the epochs: x_e = sum_j Phi_E[e][j] X_j
   for (int e = threadIdx.x; e < E; e += BIG_NTHREADS) {
     double xe[n];
@@ -236,7 +246,7 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_resid(BigArgs a, int final
       const double* Up = a.U + (long long)b * a.ustride + (long long)k * m;
       for (int c = 0; c < m; ++c) uk[c] = Up[c];
     }
-    DYN::eval(xk, uk, f, F);
+    DYN::eval(xk, uk, a.dpar, f, F);
     double W[n], V[n];
     for (int c = 0; c < n; ++c) W[c] = a.alpha * dx[c] - f[c];
     const double ck = cw[k];
@@ -294,8 +304,9 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_resid(BigArgs a, int final
         if (R == 0.0) continue;  // R = 0 masks the row (empty satellite slot, autonomous-car.py:260-263)
         double h, Gr[NA];
         MEAS::eval(xt, PR, nz, h, Gr);
-        const double ev = a.Y[(long long)b * a.M + i] - h, Re = R * ev;
+        const double yv = a.Y[(long long)b * a.M + i], ev = yv - h, Re = R * ev;
         cost += ev * Re;
+        noise += fabs(Re) * (fabs(yv) + fabs(h));
         for (int c = 0; c < n; ++c) {
           ge[c] += Gr[c] * Re;
           const double rc = R * Gr[c];
@@ -341,6 +352,7 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_resid(BigArgs a, int final
         for (int c = 0; c < p; ++c) s += R[r * p + c] * ev[c];
         Re[r] = s;
         cost += ev[r] * s;
+        noise += fabs(s) * (fabs(yi[r]) + fabs(h[r]));
       }
       for (int c = 0; c < n; ++c) {
         double s = 0.0;
@@ -389,14 +401,25 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_resid(BigArgs a, int final
   }
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   cost = wave_sum(cost);
-  if (lane == 0) red[wave] = cost;
+  noise = wave_sum(noise);
+  if (lane == 0) {
+    red[wave] = cost;
+    red[BIG_NW + wave] = noise;
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
-    double c = 0.0;
-    for (int w = 0; w < BIG_NW; ++w) c += red[w];
+    double c = 0.0, z = 0.0;
+    for (int w = 0; w < BIG_NW; ++w) {
+      c += red[w];
+      z += red[BIG_NW + w];
+    }
     a.cost[b] = c;
+    if (a.n_bounds > 0) ws[WL.NZ] = COST_NOISE * __DBL_EPSILON__ * z;
   }
-  if (a.n_bounds > 0 && !final_pass) big_active_set<n>(a, X, ws + WL.BV, (int*)(ws + WL.ACT), red);
+  if (a.n_bounds > 0 && !final_pass) {
+    big_active_set<n>(a, X, ws + WL.BV, (int*)(ws + WL.ACT), red);
+    for (int t = threadIdx.x; t < n * a.Pp; t += BIG_NTHREADS) ws[WL.GV + t] = ws[WL.BV + t];  // for the line search
+  }
 }
 
 // ------------------------------------------------------------ assembly
@@ -422,6 +445,10 @@ struct BigGSupport {
 template <int N>
 struct BigGSupport<MeasPseudorange<N>> {  // h = |x[idx0..2] - sat| + x[idx3]
   static unsigned get(const int* idx, int) { return 1u << idx[0] | 1u << idx[1] | 1u << idx[2] | 1u << idx[3]; }
+};
+template <>
+struct BigGSupport<MeasVehiclePseudorange> {  // h = |x[0, 1, 8] - sat| + x[6]
+  static unsigned get(const int*, int) { return 1u << 0 | 1u << 1 | 1u << 8 | 1u << 6; }
 };
 
 constexpr int BIG_PCH = 5;  // pair accumulators per wave (96 VGPRs, no spills)
@@ -1054,19 +1081,19 @@ struct MeasArgLen<MEAS, n, true> {
 };
 
 template <class DYN, class MEAS>
-__device__ double big_cost(const BigArgs& a, const double* X, int b, double* red) {
+__device__ double big_cost(const BigArgs& a, const double* X, int b, double* red, double& nz_out) {
   constexpr int n = DYN::n, m = DYN::m, p = MEAS::p, q = MEAS::q, NAX = MeasArgLen<MEAS, n>::v;
   const BigConst CL = big_const_layout(a.P, a.M, n, p, a.nc);
   const double* Dt = (const double*)(a.cbuf + CL.Dt);
   const double* cw = (const double*)(a.cbuf + CL.cw);
   const double* Qw = (const double*)(a.cbuf + CL.Qw);
   const double* Pw = (const double*)(a.cbuf + CL.Pw);
-  const double* Rw = (const double*)(a.cbuf + CL.Rw);
+  const double* Rw = big_rw(a, (const double*)(a.cbuf + CL.Rw), b);
   const double* PhiET = (const double*)(a.cbuf + CL.PhiET);
   const int* erow = (const int*)(a.cbuf + CL.erow);
   const int E = a.M > 0 ? *(const int*)(a.cbuf + CL.ne) : 0;
   const int Mr = a.M > 0 ? a.M : 1;
-  double cost = 0.0;
+  double cost = 0.0, noise = 0.0;
   for (int k = threadIdx.x; k < a.P; k += BIG_NTHREADS) {
     double dx[n], xk[n], uk[m > 0 ? m : 1], f[n], F[n * n];
     for (int c = 0; c < n; ++c) dx[c] = 0.0;
@@ -1079,7 +1106,7 @@ __device__ double big_cost(const BigArgs& a, const double* X, int b, double* red
       const double* Up = a.U + (long long)b * a.ustride + (long long)k * m;
       for (int c = 0; c < m; ++c) uk[c] = Up[c];
     }
-    DYN::eval(xk, uk, f, F);
+    DYN::eval(xk, uk, a.dpar, f, F);
     double W[n];
     for (int c = 0; c < n; ++c) W[c] = a.alpha * dx[c] - f[c];
     const double ck = cw[k];
@@ -1103,8 +1130,9 @@ __device__ double big_cost(const BigArgs& a, const double* X, int b, double* red
         if (R == 0.0) continue;
         double h, Gr[NAX];
         MEAS::eval(xe, PR, 0, h, Gr);
-        const double ev = a.Y[(long long)b * a.M + i] - h;
+        const double yv = a.Y[(long long)b * a.M + i], ev = yv - h;
         cost += ev * (R * ev);
+        noise += fabs(R * ev) * (fabs(yv) + fabs(h));
       } else {
         double par[q > 0 ? q : 1];
         if (q > 0) {
@@ -1122,6 +1150,7 @@ __device__ double big_cost(const BigArgs& a, const double* X, int b, double* red
           double s = 0.0;
           for (int c = 0; c < p; ++c) s += R[r * p + c] * ev[c];
           cost += ev[r] * s;
+          noise += fabs(s) * (fabs(yi[r]) + fabs(h[r]));
         }
       }
     }
@@ -1135,12 +1164,20 @@ __device__ double big_cost(const BigArgs& a, const double* X, int b, double* red
   }
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   cost = wave_sum(cost);
+  noise = wave_sum(noise);
   __syncthreads();
-  if (lane == 0) red[wave] = cost;
+  if (lane == 0) {
+    red[wave] = cost;
+    red[BIG_NW + wave] = noise;
+  }
   __syncthreads();
-  double c = 0.0;
-  for (int w = 0; w < BIG_NW; ++w) c += red[w];
+  double c = 0.0, z = 0.0;
+  for (int w = 0; w < BIG_NW; ++w) {
+    c += red[w];
+    z += red[BIG_NW + w];
+  }
   __syncthreads();
+  nz_out = COST_NOISE * __DBL_EPSILON__ * z;
   return c;
 }
 
@@ -1155,7 +1192,7 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_linesearch(BigArgs a) {
   const BigWs WL = big_ws_layout(a.P, a.M, n, a.NT, a.nz, a.nc);
   const double* ws = a.ws + (size_t)b * a.ws_stride;
   const double* YV = ws + WL.YV;
-  const double* BV = ws + WL.BV;
+  const double* GV = ws + WL.GV;  // -g at X (k_big_resid; BV now holds the forward solve)
   const int* ACT = (const int*)(ws + WL.ACT);
   double* X = a.X + (size_t)b * a.P * n;
   extern __shared__ __attribute__((aligned(16))) double xt[];  // trial iterate (P, n)
@@ -1175,6 +1212,7 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_linesearch(BigArgs a) {
     return;
   }
   const double cost0 = a.cost[b];  // k_big_resid at X
+  const double nz0 = ws[WL.NZ];    // its rounding level (Armijo slack, as k_gn_bounded)
   double alpha = 1.0;
   for (int ls = 0;;) {
     double pred = 0.0;
@@ -1183,13 +1221,14 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_linesearch(BigArgs a) {
       double lo, hi;
       big_box(a, c, lo, hi);
       const int u = c * a.Pp + j;
-      const double x = X[t], dv = YV[u], g = -BV[u];
+      const double x = X[t], dv = YV[u], g = -GV[u];
       const double xv = fmin(fmax(x + alpha * dv, lo), hi);
       pred += ACT[u] ? g * (xv - x) : alpha * g * dv;
       xt[t] = xv;
     }
     __syncthreads();
-    const double ct = big_cost<DYN, MEAS>(a, xt, b, red);
+    double nzt;
+    const double ct = big_cost<DYN, MEAS>(a, xt, b, red, nzt);
     pred = wave_sum(pred);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = pred;
     __syncthreads();
@@ -1197,7 +1236,7 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_linesearch(BigArgs a) {
     for (int w = 0; w < BIG_NW; ++w) pred += red[w];
     __syncthreads();
     ++ls;
-    if (ct <= cost0 + 2.0 * 1e-4 * pred + 1e-12 * fabs(cost0) || ls >= 30) break;  // ARMIJO_SIGMA, COST_SLACK, LS_MAX
+    if (ct <= cost0 + 2.0 * ARMIJO_SIGMA * pred + nz0 + nzt + COST_SLACK * fabs(cost0) || ls >= LS_MAX) break;
     alpha *= 0.5;
   }
   double xn = 0.0, z = 0.0;
@@ -1220,100 +1259,4 @@ __global__ void k_big_project(BigArgs a, int batch) {
   double lo, hi;
   big_box(a, (int)(t % n), lo, hi);
   a.X[t] = fmin(fmax(a.X[t], lo), hi);
-}
-
-// Every trajectory starts RUNNING -- or, when the constants buffer's stamp does not
-// match these dims, BAD_CONSTANTS: then no kernel of the solve touches the constants
-// (X_out keeps X0, cost NaN).
-__global__ void k_big_init(BigArgs a, int batch) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b < batch) {
-    const bool ok = *(const unsigned long long*)(a.cbuf + a.tag_off) == a.tag;
-    a.state[b] = ok ? BIG_RUNNING : MHE_STATUS_BAD_CONSTANTS;
-    a.iters[b] = 0;
-    if (!ok) a.cost[b] = NAN;
-  }
-}
-
-__global__ void k_big_finish(int batch, int* state) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b < batch && state[b] == BIG_RUNNING) state[b] = MHE_STATUS_MAX_ITER;
-}
-
-// ------------------------------------------------------------ constants
-__global__ void k_big_consts(int P, int M, int n, int p, const double* D, const double* cw, const double* Qw,
-                             const double* Rw, const double* Pw, char* cbuf) {
-  const BigConst CL = big_const_layout(P, M, n, p);
-  const int gid = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
-  double* oD = (double*)(cbuf + CL.D);
-  double* oDt = (double*)(cbuf + CL.Dt);
-  double* oDCD = (double*)(cbuf + CL.DCD);
-  for (int e = gid; e < P * P; e += stride) {
-    const int k = e / P, j = e % P;
-    oD[e] = D[e];
-    oDt[j * P + k] = D[e];
-    // (D^T C D)[k][j] with C = diag(cw): element (row k, col j)
-    double s = 0.0;
-    for (int t = 0; t < P; ++t) s += D[t * P + k] * cw[t] * D[t * P + j];
-    oDCD[e] = s;
-  }
-  for (int e = gid; e < P; e += stride) ((double*)(cbuf + CL.cw))[e] = cw[e];
-  for (int e = gid; e < n * n; e += stride) {
-    ((double*)(cbuf + CL.Qw))[e] = Qw[e];
-    ((double*)(cbuf + CL.Pw))[e] = Pw ? Pw[e] : 0.0;
-  }
-  for (int e = gid; e < M * p * p; e += stride) ((double*)(cbuf + CL.Rw))[e] = Rw[e];
-}
-
-// equality-constraint index pairs, passed by value (kernel arguments) so that
-// building constants stays a pure stream-ordered enqueue
-struct EqPairs {
-  int v[2 * MHE_MAX_EQ];
-};
-__global__ void k_big_eq_consts(int P, int M, int n, int p, int nc, EqPairs e, char* cbuf) {
-  const BigConst CL = big_const_layout(P, M, n, p, nc);
-  int* o = (int*)(cbuf + CL.eq);
-  for (int i = threadIdx.x; i < 2 * nc; i += blockDim.x) o[i] = e.v[i];
-}
-
-// epoch detection: row i starts an epoch unless its Phi row equals row i-1 bitwise
-__global__ void k_big_epoch_flags(int P, int M, int n, int p, const double* Phi, char* cbuf) {
-  const BigConst CL = big_const_layout(P, M, n, p);
-  int* flag = (int*)(cbuf + CL.flag);
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < M; i += gridDim.x * blockDim.x) {
-    int f = (i == 0);
-    if (!f)
-      for (int j = 0; j < P; ++j)
-        if (__double_as_longlong(Phi[(size_t)i * P + j]) != __double_as_longlong(Phi[(size_t)(i - 1) * P + j])) {
-          f = 1;
-          break;
-        }
-    flag[i] = f;
-  }
-}
-
-__global__ void k_big_epoch_scan(int P, int M, int n, int p, char* cbuf) {
-  const BigConst CL = big_const_layout(P, M, n, p);
-  const int* flag = (const int*)(cbuf + CL.flag);
-  int* erow = (int*)(cbuf + CL.erow);
-  int E = 0;
-  for (int i = 0; i < M; ++i)
-    if (flag[i]) erow[E++] = i;
-  erow[E] = M;
-  *(int*)(cbuf + CL.ne) = E;
-}
-
-__global__ void k_big_epoch_rows(int P, int M, int n, int p, const double* Phi, char* cbuf) {
-  const BigConst CL = big_const_layout(P, M, n, p);
-  const int* erow = (const int*)(cbuf + CL.erow);
-  const int E = *(const int*)(cbuf + CL.ne);
-  double* PhiE = (double*)(cbuf + CL.PhiE);
-  double* PhiET = (double*)(cbuf + CL.PhiET);
-  const int Mr = M > 0 ? M : 1;
-  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < E * P; t += gridDim.x * blockDim.x) {
-    const int e = t / P, j = t % P;
-    const double v = Phi[(size_t)erow[e] * P + j];
-    PhiE[(size_t)e * P + j] = v;
-    PhiET[(size_t)j * Mr + e] = v;
-  }
 }

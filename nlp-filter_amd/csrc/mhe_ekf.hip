@@ -394,6 +394,7 @@ extern "C" int mhe_ekf_run(const mhe_ekf_dims* dims, int32_t batch, int32_t step
                            int32_t* status, void* stream) {
   using namespace mhe_ekf;
   if (!dims) return MHE_ERR_NULL;
+  if (dims->struct_size != (int32_t)sizeof(mhe_ekf_dims)) return MHE_ERR_DIMS;  // stale / truncated binding
   if (batch < 0 || steps < 0 || dims->pmax < 1 || dims->pmax > MAXP) return MHE_ERR_DIMS;
   if (batch == 0 || steps == 0) return MHE_OK;
   if (!mu || !S || !Q || !nz || !Z || !R || (dims->m > 0 && !U)) return MHE_ERR_NULL;

@@ -153,6 +153,7 @@ extern "C" int mhe_ls_run(const mhe_ls_dims* dims, int32_t chains, int32_t epoch
                           int32_t* iters_out, double* x_last, void* stream) {
   using namespace mhe_ls;
   if (!dims) return MHE_ERR_NULL;
+  if (dims->struct_size != (int32_t)sizeof(mhe_ls_dims)) return MHE_ERR_DIMS;  // stale / truncated binding
   if (chains < 0 || epochs < 0 || dims->slots < 1 || dims->slots > 64 || dims->max_iter < 0 ||
       !(dims->tol >= 0.0))
     return MHE_ERR_DIMS;

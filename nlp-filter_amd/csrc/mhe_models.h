@@ -1,7 +1,8 @@
 // Device functors for the reference plug-ins (nlp/dynamics.py, nlp/measurements.py).
 //
-// Each dynamics functor: static n, m; eval(x, u, f, F) writes f (n) and the
-// Jacobian F = df/dx (n*n, row-major).  Each measurement functor: static p,
+// Each dynamics functor: static n, m; eval(x, u, dp, f, F) writes f (n) and the
+// Jacobian F = df/dx (n*n, row-major); dp = mhe_dims.dyn_par (the plug-in's params,
+// e.g. params["car_params"]).  Each measurement functor: static p,
 // q, LINEAR; eval(x, par, idx, h, H) writes h (p) and H = dh/dx (p*n).
 // Jacobians are analytic; their parity against the reference's own plug-ins
 // (complex-step through the reference code) is pinned by tests/golden/plugins.npz.
@@ -15,7 +16,7 @@ namespace mhe {
 // nlp/dynamics.py:4-8  xdot = u[0]
 struct DynSingleIntegrator {
   static constexpr int n = 1, m = 1;
-  __device__ static void eval(const double* x, const double* u, double* f, double* F) {
+  __device__ static void eval(const double* x, const double* u, const double*, double* f, double* F) {
     f[0] = u[0];
     F[0] = 0.0;
   }
@@ -25,7 +26,7 @@ struct DynSingleIntegrator {
 template <int N_>
 struct DynSingleIntegratorND {
   static constexpr int n = N_, m = N_;
-  __device__ static void eval(const double* x, const double* u, double* f, double* F) {
+  __device__ static void eval(const double* x, const double* u, const double*, double* f, double* F) {
 #pragma unroll
     for (int a = 0; a < n; ++a) {
       f[a] = u[a];
@@ -38,7 +39,7 @@ struct DynSingleIntegratorND {
 // nlp/dynamics.py:29-38
 struct DynDoubleIntegrator {
   static constexpr int n = 4, m = 2;
-  __device__ static void eval(const double* x, const double* u, double* f, double* F) {
+  __device__ static void eval(const double* x, const double* u, const double*, double* f, double* F) {
     f[0] = x[2]; f[1] = x[3]; f[2] = u[0]; f[3] = u[1];
 #pragma unroll
     for (int i = 0; i < 16; ++i) F[i] = 0.0;
@@ -50,7 +51,7 @@ struct DynDoubleIntegrator {
 // nlp/dynamics.py:61-66  [(1 - x1^2) x0 - x1 + u, x0]
 struct DynVanDerPol {
   static constexpr int n = 2, m = 1;
-  __device__ static void eval(const double* x, const double* u, double* f, double* F) {
+  __device__ static void eval(const double* x, const double* u, const double*, double* f, double* F) {
     const double x0 = x[0], x1 = x[1];
     const double s = 1.0 - x1 * x1;
     f[0] = s * x0 - x1 + u[0];
@@ -65,7 +66,7 @@ struct DynVanDerPol {
 // nlp/dynamics.py:68-79  [u0, u1, u2, x4, 0]
 struct DynGnssPosAndBias {
   static constexpr int n = 5, m = 3;
-  __device__ static void eval(const double* x, const double* u, double* f, double* F) {
+  __device__ static void eval(const double* x, const double* u, const double*, double* f, double* F) {
     f[0] = u[0]; f[1] = u[1]; f[2] = u[2]; f[3] = x[4]; f[4] = 0.0;
 #pragma unroll
     for (int i = 0; i < 25; ++i) F[i] = 0.0;
@@ -76,7 +77,7 @@ struct DynGnssPosAndBias {
 // nlp/dynamics.py:81-96 (m = 0: f(x, params), nlp/nlp.py:216-219)
 struct DynMultiReceiver {
   static constexpr int n = 8, m = 0;
-  __device__ static void eval(const double* x, const double*, double* f, double* F) {
+  __device__ static void eval(const double* x, const double*, const double*, double* f, double* F) {
 #pragma unroll
     for (int i = 0; i < 64; ++i) F[i] = 0.0;
 #pragma unroll
@@ -91,7 +92,7 @@ struct DynMultiReceiver {
 // nlp/dynamics.py:98-115
 struct DynGnssTwoReceiver {
   static constexpr int n = 10, m = 6;
-  __device__ static void eval(const double* x, const double* u, double* f, double* F) {
+  __device__ static void eval(const double* x, const double* u, const double*, double* f, double* F) {
     f[0] = u[0]; f[1] = u[1]; f[2] = u[2]; f[3] = x[4]; f[4] = 0.0;
     f[5] = u[3]; f[6] = u[4]; f[7] = u[5]; f[8] = x[9]; f[9] = 0.0;
 #pragma unroll
@@ -105,7 +106,7 @@ struct DynGnssTwoReceiver {
 // x[2] as the heading inside cos/sin, reproduced verbatim)
 struct DynKinematicBicycle {
   static constexpr int n = 6, m = 2;
-  __device__ static void eval(const double* x, const double* u, double* f, double* F) {
+  __device__ static void eval(const double* x, const double* u, const double*, double* f, double* F) {
     const double L = 0.28;
     const double v = 8.72649116358 * u[0] - 0.856053299155;
     const double delta = 0.48869219055841229 * u[1];  // np.deg2rad(28)
@@ -118,6 +119,55 @@ struct DynKinematicBicycle {
     F[0 * 6 + 2] = -v * sn;
     F[1 * 6 + 2] = v * cs;
     F[3 * 6 + 4] = 1.0;
+  }
+};
+
+// nlp/dynamics.py:148-174  vehicle_dynamics_and_gnss: x = [px, py, psi, vx, vy, r, b, bd, pz],
+// u = [F_xr, delta]; the dynamic bicycle of vehicle_dynamics (:148-164, linear tyres with
+// vx + 0.001 in the slip angles) plus bdot = bd.  dp = params["car_params"] as
+// [C_AF, C_AR, M, D_F, D_R, I_Z] (utils/vehicle_sim.py:10-23).
+struct DynVehicleGnss {
+  static constexpr int n = 9, m = 2;
+  __device__ static void eval(const double* x, const double* u, const double* dp, double* f, double* F) {
+    const double C_AF = dp[0], C_AR = dp[1], Mv = dp[2], D_F = dp[3], D_R = dp[4], I_Z = dp[5];
+    const double iv = 1.0 / (x[3] + 0.001);  // epsilon = .001 (nlp/dynamics.py:153)
+    const double ar = (x[4] - D_R * x[5]) * iv, af = (x[4] + D_F * x[5]) * iv;
+    const double F_yr = -C_AR * ar;
+    const double F_yf = -C_AF * (af - u[1]);
+    double sp, cp, su, cu;
+    sincos(x[2], &sp, &cp);
+    sincos(u[1], &su, &cu);
+    f[0] = x[3] * cp - x[4] * sp;
+    f[1] = x[3] * sp + x[4] * cp;
+    f[2] = x[5];
+    f[3] = (-F_yf * su + u[0]) / Mv + x[5] * x[4];
+    f[4] = (F_yf * cu + F_yr) / Mv - x[5] * x[3];
+    f[5] = (D_F * F_yf * cu - D_R * F_yr) / I_Z;
+    f[6] = x[7];
+    f[7] = 0.0;
+    f[8] = 0.0;
+#pragma unroll
+    for (int i = 0; i < 81; ++i) F[i] = 0.0;
+    // tyre forces w.r.t. vx, vy, r
+    const double fr3 = C_AR * ar * iv, fr4 = -C_AR * iv, fr5 = C_AR * D_R * iv;
+    const double ff3 = C_AF * af * iv, ff4 = -C_AF * iv, ff5 = -C_AF * D_F * iv;
+    F[0 * 9 + 2] = -x[3] * sp - x[4] * cp;
+    F[0 * 9 + 3] = cp;
+    F[0 * 9 + 4] = -sp;
+    F[1 * 9 + 2] = x[3] * cp - x[4] * sp;
+    F[1 * 9 + 3] = sp;
+    F[1 * 9 + 4] = cp;
+    F[2 * 9 + 5] = 1.0;
+    F[3 * 9 + 3] = -su * ff3 / Mv;
+    F[3 * 9 + 4] = -su * ff4 / Mv + x[5];
+    F[3 * 9 + 5] = -su * ff5 / Mv + x[4];
+    F[4 * 9 + 3] = (cu * ff3 + fr3) / Mv - x[5];
+    F[4 * 9 + 4] = (cu * ff4 + fr4) / Mv;
+    F[4 * 9 + 5] = (cu * ff5 + fr5) / Mv - x[3];
+    F[5 * 9 + 3] = (D_F * cu * ff3 - D_R * fr3) / I_Z;
+    F[5 * 9 + 4] = (D_F * cu * ff4 - D_R * fr4) / I_Z;
+    F[5 * 9 + 5] = (D_F * cu * ff5 - D_R * fr5) / I_Z;
+    F[6 * 9 + 7] = 1.0;
   }
 };
 
@@ -154,6 +204,24 @@ struct MeasPseudorange {
     H[idx[1]] += d1 * ir;
     H[idx[2]] += d2 * ir;
     H[idx[3]] += 1.0;
+  }
+};
+
+// nlp/measurements.py:81-88  vehicle_pseudorange: |[x0, x1, x8] - sat| + x6 (fixed indices)
+struct MeasVehiclePseudorange {
+  static constexpr int p = 1, q = 3;
+  static constexpr bool LINEAR = false, MIXED = false;
+  __device__ static void eval(const double* x, const double* par, const int*, double* h, double* H) {
+    const double d0 = x[0] - par[0], d1 = x[1] - par[1], d2 = x[8] - par[2];
+    const double rho = sqrt(d0 * d0 + d1 * d1 + d2 * d2);
+    h[0] = rho + x[6];
+#pragma unroll
+    for (int a = 0; a < 9; ++a) H[a] = 0.0;
+    const double ir = 1.0 / rho;
+    H[0] = d0 * ir;
+    H[1] = d1 * ir;
+    H[8] = d2 * ir;
+    H[6] = 1.0;
   }
 };
 

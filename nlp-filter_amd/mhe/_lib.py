@@ -19,26 +19,43 @@ STATUS = {0: "converged", 1: "max_iter", 2: "not_spd", 3: "nonfinite", 4: "bad_c
 c_i32, c_i64, c_dbl, c_vp, c_sz = ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p, ctypes.c_size_t
 
 
-class MheDims(ctypes.Structure):
+class _Sized(ctypes.Structure):
+    """ctypes mirror of an include/mhe.h dims struct: struct_size (first field) is set
+    to this declaration's size, which the library checks against its own sizeof."""
+
+    def __init__(self, *a, **kw):
+        super().__init__(*a, **kw)
+        self.struct_size = ctypes.sizeof(self)
+
+
+class MheDims(_Sized):
     _fields_ = [
-        ("N", c_i32), ("n", c_i32), ("m", c_i32), ("p", c_i32), ("M", c_i32), ("q", c_i32),
+        ("struct_size", c_i32), ("N", c_i32), ("n", c_i32), ("m", c_i32), ("p", c_i32), ("M", c_i32), ("q", c_i32),
         ("dyn_model", c_i32), ("meas_model", c_i32), ("has_prior", c_i32),
         ("meas_idx", c_i32 * 8), ("T", c_dbl),
         ("dyn_cost", c_i32), ("n_bounds", c_i32), ("huber_delta", c_dbl),
         ("bound_idx", c_i32 * 8), ("bound_lb", c_dbl * 8), ("bound_ub", c_dbl * 8),
         ("n_extra", c_i32), ("n_eq", c_i32), ("eq_idx", ctypes.POINTER(c_i32)),
-        ("force_large", c_i32),
+        ("force_large", c_i32), ("dyn_par", c_dbl * 8),
     ]
 
 
-class MheEkfDims(ctypes.Structure):
-    _fields_ = [("n", c_i32), ("m", c_i32), ("pmax", c_i32), ("q", c_i32),
+class MheEkfDims(_Sized):
+    _fields_ = [("struct_size", c_i32), ("n", c_i32), ("m", c_i32), ("pmax", c_i32), ("q", c_i32),
                 ("dyn_model", c_i32), ("meas_model", c_i32), ("dt", c_dbl), ("r_diag", c_i32),
                 ("hist_batch_inner", c_i32), ("in_batch_inner", c_i32)]
 
 
-class MheLsDims(ctypes.Structure):
-    _fields_ = [("slots", c_i32), ("max_iter", c_i32), ("warm", c_i32), ("with_vel", c_i32), ("tol", c_dbl)]
+class MheLsDims(_Sized):
+    _fields_ = [("struct_size", c_i32), ("slots", c_i32), ("max_iter", c_i32), ("warm", c_i32), ("with_vel", c_i32), ("tol", c_dbl)]
+
+
+class MheSolveArgs(_Sized):
+    _fields_ = [("struct_size", c_i32), ("batch", c_i32), ("X0", c_vp), ("X_out", c_vp), ("Z0", c_vp), ("Z_out", c_vp),
+                ("U", c_vp), ("u_bstride", c_i64), ("Y", c_vp), ("PAR", c_vp), ("par_bstride", c_i64),
+                ("Rw", c_vp), ("rw_bstride", c_i64), ("x0", c_vp), ("cost_out", c_vp), ("iters_out", c_vp),
+                ("status_out", c_vp), ("max_iter", c_i32), ("tol", c_dbl), ("workspace", c_vp),
+                ("workspace_bytes", c_sz)]
 
 
 _P = ctypes.POINTER(MheDims)
@@ -56,6 +73,7 @@ SIGNATURES = {
                                        c_vp, c_vp, c_vp, c_i32, c_dbl, c_vp, c_sz, c_vp]),
     "mhe_gn_solve_ext": (ctypes.c_int, [_P, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64,
                                         c_vp, c_vp, c_vp, c_vp, c_i32, c_dbl, c_vp, c_sz, c_vp]),
+    "mhe_solve": (ctypes.c_int, [_P, c_vp, ctypes.POINTER(MheSolveArgs), c_vp]),
     "mhe_assemble": (ctypes.c_int, [_P, c_vp, c_i32, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp,
                                     c_vp, c_vp, c_vp, c_vp]),
     "mhe_chol_solve": (ctypes.c_int, [_P, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),

@@ -7,7 +7,15 @@ plug-in; lookup is by the function's name within a ``dynamics`` /
 ``measurements`` module, so both this package's ``nlp.dynamics`` and the
 reference's own ``nlp/dynamics.py`` functions resolve.  An unregistered
 plug-in raises ``UnsupportedPlugin`` -- there is no CPU evaluation path.
+
+A name is not an identity: ``verify_dyn`` / ``verify_meas`` evaluate a user's
+plug-in at seeded points and compare it with this package's host definition of
+the registered plug-in (the twin of the device functor, pinned to the reference
+by tests/golden/plugins.npz), so a function that merely shares the name --
+different math, different constants -- is refused instead of silently getting
+the built-in functor.
 """
+import numpy as np
 
 DYN = {
     # name: (id, n, m)                      reference nlp/dynamics.py
@@ -20,7 +28,22 @@ DYN = {
     "multi_receiver": (7, 8, 0),            # :81-96
     "gnss_two_receiver": (8, 10, 6),        # :98-115
     "kinematic_bycicle_and_bias": (9, 6, 2),  # :117-136
+    "vehicle_dynamics_and_gnss": (10, 9, 2),  # :148-174 (params["car_params"] -> dyn_par)
 }
+
+# Static parameters of the device functors (mhe_dims.dyn_par), from the plug-in's params
+CAR_KEYS = ("C_AF", "C_AR", "M", "D_F", "D_R", "I_Z")   # utils/vehicle_sim.py:10-23
+
+
+def dyn_params(name, params):
+    """The mhe_dims.dyn_par vector of dynamics plug-in ``name`` for ``params``."""
+    out = np.zeros(8)
+    if name == "vehicle_dynamics_and_gnss":
+        if not params or "car_params" not in params:
+            raise UnsupportedPlugin("vehicle_dynamics_and_gnss needs params={'car_params': ...} (nlp/dynamics.py:151)")
+        C = params["car_params"]
+        out[:6] = [float(C[k]) for k in CAR_KEYS]
+    return out
 
 MEAS = {
     # name: (id, p, q, linear)              reference nlp/measurements.py
@@ -51,12 +74,14 @@ COMPILED_PAIRS = {
     ("gnss_pos_and_bias", "full_state"),
     ("kinematic_bycicle_and_bias", "pseudorange"),
     ("double_integrator", "full_state"),
+    ("vehicle_dynamics_and_gnss", "vehicle_pseudorange"),   # autonomous-car.py:190-213
     # mixed rows / extra variables / equality constraints (large-system path)
     ("van_der_pol", "mixed"),
     ("multi_receiver", "mixed"),
     ("gnss_two_receiver", "mixed"),
     ("gnss_pos_and_bias", "mixed"),
     ("kinematic_bycicle_and_bias", "mixed"),
+    ("vehicle_dynamics_and_gnss", "mixed"),
 }
 
 
@@ -91,3 +116,74 @@ def check_pair(dyn_name, meas_name):
         raise UnsupportedPlugin(
             f"(dynamics={dyn_name!r}, measurement={meas_name!r}) is not compiled into libmhe.so; "
             f"available: {sorted(COMPILED_PAIRS)}")
+
+
+# ---------------------------------------------------------------- identity checks
+VERIFY_POINTS = 4
+VERIFY_RTOL = 1e-12
+
+
+def _twin(kind, name):
+    import importlib
+    mod = importlib.import_module("nlp.dynamics" if kind == "dyn" else "nlp.measurements")
+    if not hasattr(mod, name):
+        raise UnsupportedPlugin(f"{kind} plug-in {name!r} has no registered twin to verify against")
+    return getattr(mod, name)
+
+
+def _close(a, b):
+    a, b = np.atleast_1d(np.asarray(a, dtype=np.float64)).ravel(), np.atleast_1d(np.asarray(b, dtype=np.float64)).ravel()
+    return a.shape == b.shape and bool(np.all(np.abs(a - b) <= VERIFY_RTOL * (1.0 + np.abs(b))))
+
+
+def _sample(rng, k, name):
+    x = rng.normal(size=k) * 3.0
+    if name == "vehicle_dynamics_and_gnss":
+        x[3] = 5.0 + abs(x[3])   # forward speed away from the tyre model's pole at vx = -0.001
+    return x
+
+
+def verify_dyn(fn, params=None):
+    """Refuse (UnsupportedPlugin) a dynamics callable whose values differ from the
+    registered plug-in of the same name at seeded points (n, m from the registry).
+    Strings and this package's own functions pass without evaluation."""
+    name, (_, n, m) = dyn_model(fn)
+    if isinstance(fn, str):
+        return
+    twin = _twin("dyn", name)
+    if fn is twin:
+        return
+    rng = np.random.default_rng(20260)
+    for _ in range(VERIFY_POINTS):
+        x = _sample(rng, n, name)
+        u = rng.normal(size=m)
+        try:
+            got = fn(x, u, params) if m > 0 else fn(x, params)
+        except Exception as e:  # symbolic-only plug-ins cannot be compared numerically
+            raise UnsupportedPlugin(f"dynamics plug-in {name!r} could not be evaluated to verify it matches the "
+                                    f"device functor: {type(e).__name__}: {e}") from e
+        ref = twin(x, u, params) if m > 0 else twin(x, params)
+        if not _close(got, ref):
+            raise UnsupportedPlugin(f"dynamics plug-in {name!r} is not the registered {name}: its values differ "
+                                    "from the device functor's (same name, different math or constants)")
+
+
+def verify_meas(fn, params, n):
+    """As verify_dyn for a measurement callable h(x, params) on an n-state."""
+    name, _ = meas_model(fn) if _name(fn) in MEAS else (_name(fn), None)
+    if isinstance(fn, str):
+        return
+    twin = _twin("meas", name)
+    if fn is twin:
+        return
+    rng = np.random.default_rng(20261)
+    for _ in range(VERIFY_POINTS):
+        x = rng.normal(size=n) * 30.0
+        try:
+            got = fn(x, params)
+        except Exception as e:
+            raise UnsupportedPlugin(f"measurement plug-in {name!r} could not be evaluated to verify it matches the "
+                                    f"device functor: {type(e).__name__}: {e}") from e
+        if not _close(got, twin(x, params)):
+            raise UnsupportedPlugin(f"measurement plug-in {name!r} is not the registered {name}: its values differ "
+                                    "from the device functor's (same name, different math or constants)")

@@ -10,6 +10,9 @@ tensor the launch touches is kept alive for it -- mhe.streams).  The large-syste
 workspace is cached per stream, so concurrent solves on different streams never
 share one.
 """
+import collections
+import ctypes
+
 import numpy as np
 import torch
 
@@ -65,11 +68,17 @@ class BatchSolver:
                       vector (b = -1: v[a] = 0), met by every GN step (bordered KKT solve)
       force_large     take the large-system path even when the register-resident kernel
                       fits (parity tests of the two paths; fixed at construction)
+      dyn_par         static dynamics parameters (mhe_dims.dyn_par; registry.dyn_params turns a
+                      plug-in's params dict into it, e.g. car_params for vehicle_dynamics_and_gnss)
     With meas="mixed", PAR rows follow include/mhe.h (q = 14) and Rw is (M,) weights.
     """
 
+    WS_CACHE = 2  # large-system workspaces kept alive (one per recently used stream)
+    ws_budget = None  # bytes of workspace one launch may use (None: 85 % of the free HBM)
+
     def __init__(self, N, T, dyn, meas, D, cw, Phi, Qw, Rw, Pw=None, meas_idx=None, device="cuda",
-                 dyn_cost="l2", huber_delta=None, bounds=None, n_extra=0, eq=None, force_large=False):
+                 dyn_cost="l2", huber_delta=None, bounds=None, n_extra=0, eq=None, force_large=False,
+                 dyn_par=None):
         self.lib = _lib.load()
         if not torch.cuda.is_available():
             raise _lib.MheLibraryError("no HIP device visible: the estimator has no CPU path")
@@ -87,7 +96,7 @@ class BatchSolver:
         dims.N, dims.n, dims.m, dims.p, dims.M, dims.q = self.N, n, m, p, self.M, q
         dims.dyn_model, dims.meas_model = did, mid
         dims.has_prior = 0 if Pw is None else 1
-        idx = list(meas_idx) if meas_idx is not None else ([0, 1, 2, 3] if mname != "vehicle_pseudorange" else [0, 1, 8, 6])
+        idx = list(meas_idx) if meas_idx is not None else [0, 1, 2, 3]
         for i in range(8):
             dims.meas_idx[i] = idx[i] if i < len(idx) else 0
         dims.T = self.T
@@ -116,6 +125,12 @@ class BatchSolver:
             dims.eq_idx = self._eq.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))  # self._eq keeps it alive
         self.n_eq = dims.n_eq
         dims.force_large = 1 if force_large else 0
+        if dyn_par is None and dname == "vehicle_dynamics_and_gnss":
+            raise ValueError("vehicle_dynamics_and_gnss needs dyn_par (registry.dyn_params(name, params))")
+        dp = np.zeros(8) if dyn_par is None else np.asarray(dyn_par, dtype=np.float64).ravel()
+        for i in range(8):
+            dims.dyn_par[i] = float(dp[i]) if i < dp.size else 0.0
+        self.dyn_par = dp
         self.dims = dims
         self.dp = self.lib.mhe_padded_dim(dims)
         if self.dp < 0:
@@ -130,7 +145,7 @@ class BatchSolver:
         self._src = {k: _dev(v, dev) for k, v in self._host.items() if v is not None}
         self.cbuf = torch.empty(nbytes, dtype=torch.uint8, device=dev)
         Pw_t = self._src.get("Pw")
-        self._ws = {}  # large-system workspace per stream handle
+        self._ws = collections.OrderedDict()  # large-system workspace per stream handle (LRU, <= WS_CACHE)
         cur = torch.cuda.current_stream(dev)
         rc = self.lib.mhe_build_constants(
             self.dims, _ptr(self._src["D"]), _ptr(self._src["cw"]), _ptr(self._src["Phi"]),
@@ -176,34 +191,99 @@ class BatchSolver:
         mhe_gn_solve_ws then needs a device workspace (allocated here, cached)."""
         return self.lib.mhe_workspace_bytes(self.dims, 1) > 0
 
+    def _chunk(self, B):
+        """Trajectories per launch on the large-system path: all B unless their
+        workspace exceeds the budget (ws_budget bytes, default 85 % of the free HBM
+        plus what this solver already holds) -- then the batch is streamed in equal
+        chunks through one workspace (C5: 2048 trajectories x 0.28 GB)."""
+        per = self.lib.mhe_workspace_bytes(self.dims, 1)
+        if per == 0 or B == 0:
+            return B
+        budget = self.ws_budget
+        if budget is None:
+            free, _ = torch.cuda.mem_get_info(self.device)
+            budget = int(0.85 * (free + sum(w.numel() for w in self._ws.values())))
+        k = max(1, min(B, budget // per))
+        nch = -(-B // k)
+        return -(-B // nch)  # equal chunks
+
     def _workspace(self, B, s):
         """Workspace for B trajectories on stream s (allocated on s: one per stream, so
         concurrent solves on different streams never share or free each other's)."""
         nb = self.lib.mhe_workspace_bytes(self.dims, B)
         if nb == 0:
             return None, 0
-        ws = self._ws.get(s.cuda_stream)
+        key = s.cuda_stream
+        ws = self._ws.pop(key, None)
         if ws is None or ws.numel() < nb:
+            ws = None  # release the old one before allocating the larger one
             ws = torch.empty(nb, dtype=torch.uint8, device=self.device)
-            self._ws[s.cuda_stream] = ws
+        self._ws[key] = ws  # most recently used last
+        while len(self._ws) > self.WS_CACHE:
+            # dropping the reference is safe: a launch on another stream recorded its
+            # workspace on that stream (keep_alive), so the allocator reuses it only
+            # after that stream's work is done
+            self._ws.popitem(last=False)
         return ws, nb
 
+    def _rw(self, Rw, B):
+        """Per-solve measurement weights (mhe_solve_args.Rw): (B|1, M, p, p), or (B|1, M)
+        for mixed rows; None = the weights the constants were built with."""
+        if Rw is None:
+            return None, 0
+        if self.linear_meas:
+            raise ValueError("per-solve Rw needs a nonlinear measurement model (a linear h folds R into the constants)")
+        shape = (self.M,) if self.meas_name == "mixed" else (self.M, self.p, self.p)
+        t = _dev(Rw, self.device)
+        if t.shape == shape:
+            t = t[None]
+        if t.shape[1:] != shape or t.shape[0] not in (1, B):
+            raise ValueError(f"Rw must be (B|1,) + {shape}, got {tuple(t.shape)}")
+        return t, (0 if t.shape[0] == 1 else int(np.prod(shape)))
+
     def _gn(self, s, cur, B, X, Xo, U_t, ustr, Y_t, PAR_t, pstr, x0_t, cost, iters, status, max_iter, tol,
-            Z=None, Zo=None):
-        ws, nb = self._workspace(B, s)
-        rc = self.lib.mhe_gn_solve_ext(self.dims, _ptr(self.cbuf), B, _ptr(X), _ptr(Xo), _ptr(Z), _ptr(Zo),
-                                       _ptr(U_t), ustr, _ptr(Y_t), _ptr(PAR_t), pstr, _ptr(x0_t), _ptr(cost),
-                                       _ptr(iters), _ptr(status), int(max_iter), float(tol), _ptr(ws), nb,
-                                       _handle(s))
-        _lib.check(rc, "mhe_gn_solve_ext")
-        keep_alive(s, cur, X, Xo, Z, Zo, U_t, Y_t, PAR_t, x0_t, cost, iters, status, ws)
+            Z=None, Zo=None, Rw=None):
+        Rw_t, rstr = self._rw(Rw, B)
+        if B == 0:
+            return
+        chunk = self._chunk(B)
+        ws, nb = self._workspace(chunk, s)
+        P, n, M = self.P, self.n, self.M
+        for lo in range(0, B, chunk):
+            c = min(chunk, B - lo)
+            a = _lib.MheSolveArgs()
+
+            def at(t, per, stride=None):
+                if t is None:
+                    return None
+                st = per if stride is None else stride
+                return ctypes.c_void_p(t.data_ptr() + 8 * lo * st) if st else ctypes.c_void_p(t.data_ptr())
+
+            a.batch = c
+            a.X0, a.X_out = at(X, P * n), at(Xo, P * n)
+            a.Z0, a.Z_out = at(Z, self.n_extra), at(Zo, self.n_extra)
+            a.U, a.u_bstride = at(U_t, 0, ustr), ustr
+            a.Y = at(Y_t, M * self.p)
+            a.PAR, a.par_bstride = at(PAR_t, 0, pstr), pstr
+            a.Rw, a.rw_bstride = at(Rw_t, 0, rstr), rstr
+            a.x0 = at(x0_t, n)
+            a.cost_out = at(cost, 1)
+            a.iters_out = ctypes.c_void_p(iters.data_ptr() + 4 * lo)
+            a.status_out = ctypes.c_void_p(status.data_ptr() + 4 * lo)
+            a.max_iter, a.tol = int(max_iter), float(tol)
+            a.workspace, a.workspace_bytes = (None if ws is None else ctypes.c_void_p(ws.data_ptr())), nb
+            rc = self.lib.mhe_solve(self.dims, _ptr(self.cbuf), ctypes.byref(a), _handle(s))
+            _lib.check(rc, "mhe_solve")
+        keep_alive(s, cur, X, Xo, Z, Zo, U_t, Y_t, PAR_t, Rw_t, x0_t, cost, iters, status, ws)
 
     # ------------------------------------------------------------------ calls
-    def solve(self, X0, U, Y, PAR=None, x0=None, max_iter=20, tol=1e-10, stream=None, out=None, Z0=None):
+    def solve(self, X0, U, Y, PAR=None, x0=None, max_iter=20, tol=1e-10, stream=None, out=None, Z0=None, Rw=None):
         """Gauss-Newton to convergence. Returns (X, cost, iters, status) device tensors,
         and the extra variables Z (B, n_extra) as a fifth element when n_extra > 0.
-        With ``stream`` the work (staging included) is ordered on that stream; consume
-        the outputs there or make the consuming stream wait for it."""
+        ``Rw`` (B|1, M, p, p) -- (B|1, M) for mixed rows -- replaces the measurement
+        weights of the constants for this solve (nonlinear models; the MHE windows'
+        R = 0 slot masks).  With ``stream`` the work (staging included) is ordered on
+        that stream; consume the outputs there or make the consuming stream wait for it."""
         with launch_stream(stream, self.device, (self._built,)) as (s, cur):
             X, B, U_t, ustr, Y_t, PAR_t, pstr, x0_t = self._inputs(X0, U, Y, PAR, x0)
             if out is None:
@@ -217,7 +297,8 @@ class BatchSolver:
             if self.n_extra:
                 Z = _dev(np.zeros((B, self.n_extra)) if Z0 is None else Z0, self.device, (B, self.n_extra))
                 Zo = torch.empty_like(Z)
-            self._gn(s, cur, B, X, Xo, U_t, ustr, Y_t, PAR_t, pstr, x0_t, cost, iters, status, max_iter, tol, Z, Zo)
+            self._gn(s, cur, B, X, Xo, U_t, ustr, Y_t, PAR_t, pstr, x0_t, cost, iters, status, max_iter, tol, Z, Zo,
+                     Rw)
         if self.n_extra:
             return Xo, cost, iters, status, Zo
         return Xo, cost, iters, status
@@ -266,5 +347,7 @@ def from_workload(w, device="cuda", **kw):
     """BatchSolver for a mhe.configs.Workload (kw: dyn_cost, huber_delta, bounds)."""
     Phi = w.cpm.lagrange_matrix(w.t_meas)
     kw.setdefault("n_extra", getattr(w, "n_extra", 0))
+    if getattr(w, "dyn_par", None) is not None:
+        kw.setdefault("dyn_par", w.dyn_par)
     return BatchSolver(w.N, w.T, w.dyn, w.meas, w.cpm.D, (w.T / 2.0) * w.cpm.w, Phi, w.Qw, w.Rw,
                        Pw=w.Pw, meas_idx=w.meas_static.get("idx"), device=device, **kw)

@@ -55,3 +55,24 @@ def kinematic_bycicle_and_bias(x, u, params=None):
     v = 8.72649116358 * u[0] - 0.856053299155
     delta = np.deg2rad(28) * u[1]
     return vertcat(v * cos(x[2]), v * sin(x[2]), 0.0, x[4], 0.0, (v / L) * tan(delta))
+
+
+def vehicle_dynamics(x, u, params=None):
+    """Dynamic bicycle with linear tyres, x = [px, py, psi, vx, vy, r],
+    u = [F_xr, delta]; C = params["car_params"]  (nlp/dynamics.py:148-164)."""
+    C = params["car_params"]
+    epsilon = .001
+    F_yr = -C["C_AR"] * (x[4] - C["D_R"] * x[5]) / (x[3] + epsilon)
+    F_yf = -C["C_AF"] * ((x[4] + C["D_F"] * x[5]) / (x[3] + epsilon) - u[1])
+    return vertcat(x[3] * cos(x[2]) - x[4] * sin(x[2]),
+                   x[3] * sin(x[2]) + x[4] * cos(x[2]),
+                   x[5],
+                   (-F_yf * sin(u[1]) + u[0]) / C["M"] + x[5] * x[4],
+                   (F_yf * cos(u[1]) + F_yr) / C["M"] - x[5] * x[3],
+                   (C["D_F"] * F_yf * cos(u[1]) - C["D_R"] * F_yr) / C["I_Z"])
+
+
+def vehicle_dynamics_and_gnss(x, u, params=None):
+    """x = [px, py, psi, vx, vy, psid, b, bd, pz]: vehicle_dynamics plus bdot = bd
+    (nlp/dynamics.py:166-174; autonomous-car.py:192)."""
+    return vertcat(vehicle_dynamics(x[:6], u, params), x[7], 0.0, 0.0)

@@ -466,11 +466,45 @@ class fixedTimeOptimalEstimationNLP(NLP):
         except ParameterNotSet:
             self._engine_key = None
 
+    def _verify_plugins(self):
+        """Each user plug-in is checked once against the registered plug-in of its
+        name (mhe.registry.verify_dyn / verify_meas): same values at seeded points,
+        or UnsupportedPlugin -- a name alone does not select a device functor."""
+        from mhe import registry
+        done = self.__dict__.setdefault("_verified", set())
+        rng = np.random.default_rng(7)
+
+        def num(params):
+            out = {}
+            for k, v in (params or {}).items():
+                if isinstance(v, Param):
+                    out[k] = v.get()
+                elif isinstance(v, Var):
+                    out[k] = rng.normal(size=v.size) * 10.0   # an extra decision variable: any value
+                else:
+                    out[k] = v
+            return out
+
+        func, dparams = self._dyn[0], self._dyn[1]
+        if id(func) not in done:
+            registry.verify_dyn(func, num(dparams))
+            done.add(id(func))
+        for g in self._meas:
+            h = g["h"]
+            if id(h) in done:
+                continue
+            registry.verify_meas(h, num(g["params"]), self.n)
+            done.add(id(h))
+
     def _build(self):
+        from mhe import registry
         from mhe import solver as _solver
         if self._dyn is None or self._dyn_cost is None or not self._meas:
             self._spec()  # raises the precise error
+        self._verify_plugins()
         func = self._dyn[0]
+        dname = _fname(func)
+        dyn_par = registry.dyn_params(dname, self._dyn[1]) if dname in registry.DYN else None
         Pw = None if self._prior is None else np.asarray(_resolve(self._prior[0]), dtype=np.float64)
         bounds = self._enforced_bounds()
         huber = getattr(self, "_huber", None)
@@ -488,14 +522,21 @@ class fixedTimeOptimalEstimationNLP(NLP):
             mname, t_meas, Rw, PAR, idx = self._spec()
             self._Ymixed = None
         Phi = self.CPM.lagrange_matrix(t_meas)
-        key = (mname, t_meas.tobytes(), Rw.tobytes(), None if Pw is None else Pw.tobytes(), self._dyn_cost.tobytes(),
-               huber, tuple(bounds), nz, None if eq is None else eq.tobytes())
+        # R enters the device constants only for a linear h (folded into J^T W J); a
+        # nonlinear model takes it per solve (mhe_solve_args.Rw), so re-setting R every
+        # window -- the R = 0 slot masks of autonomous-car.py:250-263 -- reuses the engine
+        linear = registry.MEAS[mname][3]
+        key = (mname, t_meas.tobytes(), Rw.tobytes() if linear else Rw.shape, None if Pw is None else Pw.tobytes(),
+               self._dyn_cost.tobytes(), huber, tuple(bounds), nz, None if eq is None else eq.tobytes(),
+               None if dyn_par is None else dyn_par.tobytes())
         if self._engine is None or self._engine_key != key:
             self._engine = _solver.BatchSolver(self.N, self.T, func, mname, self.CPM.D, (self.T / 2.0) * self.CPM.w,
                                                Phi, self._dyn_cost, Rw, Pw=Pw, meas_idx=idx, device=self.device,
                                                dyn_cost="huber" if huber is not None else "l2", huber_delta=huber,
-                                               bounds=bounds, n_extra=nz, eq=eq)
+                                               bounds=bounds, n_extra=nz, eq=eq, dyn_par=dyn_par)
             self._engine_key = key
+            self.engine_builds = getattr(self, "engine_builds", 0) + 1
+        self._Rw_solve = None if linear else Rw
         self._PAR = PAR
         self._extra = extra
 
@@ -537,7 +578,8 @@ class fixedTimeOptimalEstimationNLP(NLP):
         x0 = None if self._prior is None else self._prior[1].get()[None]
         import torch
         t0 = time.perf_counter()
-        out = eng.solve(X0, U, Y, PAR, x0, max_iter=self.max_iter, tol=self.tol, Z0=Z0)
+        Rw = None if self._Rw_solve is None else self._Rw_solve[None]
+        out = eng.solve(X0, U, Y, PAR, x0, max_iter=self.max_iter, tol=self.tol, Z0=Z0, Rw=Rw)
         X, cost, iters, status = out[:4]
         torch.cuda.synchronize()
         t_wall = time.perf_counter() - t0

@@ -36,7 +36,7 @@ class Problem:
     """Structure shared by every trajectory of a batch (plain container)."""
 
     def __init__(self, N, T, n, m, dyn, meas, D, c, Phi, Qw, Rw, Pw=None, meas_static=None,
-                 dyn_cost="l2", delta=None, lb=None, ub=None):
+                 dyn_cost="l2", delta=None, lb=None, ub=None, dyn_par=None):
         self.N, self.T, self.n, self.m = N, float(T), n, m
         # dynamics cost: "l2" = weighted_l2_norm, "huber" = pseudo_huber_loss with params
         # {"Q": Qw, "delta": delta} (cost_functions.py:20-31; only diag(Qw) enters the Huber)
@@ -48,6 +48,7 @@ class Problem:
         self.d = self.P * n
         self.alpha = 2.0 / float(T)
         self.dyn, self.meas = dyn, meas
+        self.dyn_par = dyn_par                            # the dynamics plug-in's params (car_params)
         self.meas_static = meas_static or {}
         self.D = np.asarray(D, dtype=np.float64)
         self.c = np.asarray(c, dtype=np.float64)          # (T/2) w_k
@@ -62,7 +63,7 @@ def residuals(pb, X, U, Y, PAR=None, x0=None):
     """Return W (B,P,n), xi (B,M,n), e (B,M,p), cost (B,)."""
     X = np.asarray(X, dtype=np.float64)
     DX = np.einsum("kj,bja->bka", pb.D, X)
-    f, _ = models.dyn_eval(pb.dyn, X, U)
+    f, _ = models.dyn_eval(pb.dyn, X, U, pb.dyn_par)
     W = pb.alpha * DX - f
     if pb.dyn_cost == "huber":  # sum_i 2 Q_ii delta^2 (sqrt(1 + W_i^2/delta^2) - 1), cost_functions.py:25-31
         q, dl = np.diag(pb.Qw), pb.delta
@@ -79,6 +80,25 @@ def residuals(pb, X, U, Y, PAR=None, x0=None):
         r0 = X[:, 0] - x0
         cost = cost + np.einsum("ba,ac,bc->b", r0, pb.Pw, r0)
     return W, xi, e, cost
+
+
+def cost_noise(pb, X, U, Y, PAR=None, x0=None):
+    """Rounding level of the cost at X (B,): e = y - h(x) carries eps (|y| + |h|) of
+    rounding in any evaluation order, so cost = sum e^T R e carries up to
+    2 |R e| eps (|y| + |h|) per row -- with pseudoranges (|y| ~ 2e7 m) far above
+    1e-12 |cost|.  Twice that bound (COST_NOISE) enters the Armijo test of the
+    projected Newton method: a decrease below the rounding level cannot be resolved,
+    so it must not be demanded (else the search shrinks the step to zero there)."""
+    X = np.asarray(X, dtype=np.float64)
+    xi = np.einsum("ij,bja->bia", pb.Phi, X)
+    h, _ = models.meas_eval(pb.meas, xi, PAR, pb.meas_static)
+    Rw = pb.Rw if pb.Rw.ndim == 4 else pb.Rw[None]
+    mask = masked_rows(Rw)[..., None]
+    with np.errstate(invalid="ignore"):
+        e = np.where(mask, 0.0, Y - h)
+        mag = np.where(mask, 0.0, np.abs(Y) + np.abs(h))
+    Re = np.einsum("bipq,biq->bip", np.broadcast_to(Rw, e.shape + (e.shape[-1],)), e)
+    return COST_NOISE * np.finfo(np.float64).eps * np.einsum("bip,bip->b", np.abs(Re), mag)
 
 
 def masked_rows(Rw):
@@ -107,7 +127,7 @@ def normal_equations(pb, X, U, Y, PAR=None, x0=None):
     X = np.asarray(X, dtype=np.float64)
     B, P, n = X.shape
     W, xi, e, cost = residuals(pb, X, U, Y, PAR, x0)
-    _, F = models.dyn_eval(pb.dyn, X, U)
+    _, F = models.dyn_eval(pb.dyn, X, U, pb.dyn_par)
     a = pb.alpha
     # dynamics: block(j,l) = a^2 (D^T C D)_jl Qw - a D_lj E_l - a D_jl E_j^T + delta_jl F_j^T E_j
     if pb.dyn_cost == "huber":
@@ -163,7 +183,7 @@ def normal_equations_explicit(pb, X, U, Y, PAR=None, x0=None):
     for b in range(B):
         rows, Ws, rs = [], [], []
         for k in range(P):  # dynamics defect rows, nlp/nlp.py:225-235
-            fk, Fk = models.dyn_eval(pb.dyn, X[b, k], None if U is None else U[b, k])
+            fk, Fk = models.dyn_eval(pb.dyn, X[b, k], None if U is None else U[b, k], pb.dyn_par)
             Wk = pb.alpha * (pb.D[k] @ X[b]) - fk
             A = np.zeros((n, d))
             for j in range(P):
@@ -204,7 +224,7 @@ def normal_equations_explicit(pb, X, U, Y, PAR=None, x0=None):
     return np.stack(Hs), np.stack(gs), np.array(cs)
 
 
-def gauss_newton(pb, X0, U, Y, PAR=None, x0=None, max_iter=20, tol=1e-10):
+def gauss_newton(pb, X0, U, Y, PAR=None, x0=None, max_iter=20, tol=1e-10, trace=None):
     """Batched GN with the same stopping rule as the HIP kernel.
 
     Per trajectory: solve H delta = -g (Cholesky), X += delta, iters += 1;
@@ -214,7 +234,7 @@ def gauss_newton(pb, X0, U, Y, PAR=None, x0=None, max_iter=20, tol=1e-10):
     ``gauss_newton_bounded``.
     """
     if pb.lb is not None or pb.ub is not None:
-        return gauss_newton_bounded(pb, X0, U, Y, PAR, x0, max_iter, tol)
+        return gauss_newton_bounded(pb, X0, U, Y, PAR, x0, max_iter, tol, trace)
     X = np.array(X0, dtype=np.float64, copy=True)
     B = X.shape[0]
     iters = np.zeros(B, dtype=np.int32)
@@ -260,6 +280,7 @@ ARMIJO_SIGMA = 1e-4  # sufficient decrease along the projection arc
 LS_MAX = 30          # step halvings; the last trial is taken if none is accepted
 COST_SLACK = 1e-12   # relative cost slack of the Armijo test: near a solution the decrease
                      # falls below the cost's rounding error and full steps must pass
+COST_NOISE = 4.0     # cost_noise: 2 (d cost / d e) x 2 (margin) eps |R e| (|y| + |h|) per row
 
 
 def box(pb, shape):
@@ -281,7 +302,7 @@ def active_set(pb, X, g):
     return bounded & (((X <= lo + eps) & (g > 0)) | ((X >= hi - eps) & (g < 0)))
 
 
-def gauss_newton_bounded(pb, X0, U, Y, PAR=None, x0=None, max_iter=20, tol=1e-10):
+def gauss_newton_bounded(pb, X0, U, Y, PAR=None, x0=None, max_iter=20, tol=1e-10, trace=None):
     """Gauss-Newton with bounds as a projected Newton method (per trajectory):
 
       X <- P(X0)                                   (P: projection onto the box)
@@ -293,10 +314,12 @@ def gauss_newton_bounded(pb, X0, U, Y, PAR=None, x0=None, max_iter=20, tol=1e-10
         s  = P(X + d) - X                           (stationarity: s = 0 at a KKT point)
         a = 1, 1/2, ... (LS_MAX trials): X(a) = P(X + a d) until
           cost(X(a)) <= cost(X) + 2 sigma [sum_free a g.d + sum_A g.(X(a) - X)]
-                         + COST_SLACK |cost(X)|
+                         + noise(X) + noise(X(a)) + COST_SLACK |cost(X)|
+        (noise: cost_noise, the rounding level of the cost at that point)
         X <- X(a);  converged when max|s| <= tol (1 + max|X|).
     Limit points are KKT points of the bound-constrained least-squares problem (the
-    fixed point of plain step clipping is not).  Returns X, cost, iters, status."""
+    fixed point of plain step clipping is not).  Returns X, cost, iters, status.
+    ``trace`` (a list) receives (trajectory, iteration, accepted alpha) per step."""
     X = np.array(X0, dtype=np.float64, copy=True)
     B = X.shape[0]
     lo, hi = box(pb, X.shape[1:])
@@ -337,14 +360,18 @@ def gauss_newton_bounded(pb, X0, U, Y, PAR=None, x0=None, max_iter=20, tol=1e-10
             actr = act.reshape(x.shape)
             gr = g.reshape(x.shape)
             alpha = 1.0
+            nz0 = cost_noise(pbs, Xb, *args)[0]
             for _ in range(LS_MAX):
                 xt = np.clip(x + alpha * d, lo, hi)
                 pred = alpha * np.sum(np.where(actr, 0.0, gr * d)) + np.sum(np.where(actr, gr * (xt - x), 0.0))
                 Jt = residuals(pbs, xt[None], *args)[3][0]
-                if Jt <= J + 2.0 * ARMIJO_SIGMA * pred + COST_SLACK * abs(J):
+                nzt = cost_noise(pbs, xt[None], *args)[0]
+                if Jt <= J + 2.0 * ARMIJO_SIGMA * pred + nz0 + nzt + COST_SLACK * abs(J):
                     break
                 alpha *= 0.5
             Xb = xt[None]
+            if trace is not None:
+                trace.append((b, int(iters[b]), alpha))
             iters[b] += 1
             if np.max(np.abs(s)) <= tol * (1.0 + np.max(np.abs(xt))):
                 status[b] = OK
@@ -408,7 +435,7 @@ class CpuPort:
         B, P, n = X.shape
         d = P * n
         W, xi, e, cost = residuals(pb, X, U, Y, None, x0)
-        _, F = models.dyn_eval(pb.dyn, X, U)
+        _, F = models.dyn_eval(pb.dyn, X, U, pb.dyn_par)
         E = np.einsum("k,ac,zkce->zkae", pb.c, pb.Qw, F)
         # M[(j,a),(l,e)] = D_lj E_l[a,e];  H = Hc - a (M + M^T) + blkdiag(F^T E)
         Mx = (pb.D.T[None, :, None, :, None] * E.transpose(0, 2, 1, 3)[:, None]).reshape(B, d, d)

@@ -13,6 +13,9 @@ Dynamics  f(x, u) -> (f (..., n), F = df/dx (..., n, n))
   gnss_two_receiver            nlp/dynamics.py:98-115
   kinematic_bycicle_and_bias   nlp/dynamics.py:117-136 (uses x[2] as the heading,
                                exactly as the reference code does)
+  vehicle_dynamics_and_gnss    nlp/dynamics.py:148-174 (static = params["car_params"]:
+                               a dict with C_AF, C_AR, M, D_F, D_R, I_Z as
+                               utils/vehicle_sim.py:10-23, or that 6-vector)
 
 Measurements  h(x, par) -> (h (..., p), H = dh/dx (..., p, n))
   full_state                   nlp/measurements.py:4-5
@@ -74,6 +77,41 @@ def dyn_eval(name, x, u, static=None):
         F[..., 0, 2] = -v * np.sin(x[..., 2])
         F[..., 1, 2] = v * np.cos(x[..., 2])
         F[..., 3, 4] = 1.0
+    elif name == "vehicle_dynamics_and_gnss":
+        C = static
+        if isinstance(C, dict):
+            C = C.get("car_params", C)
+            C = [C["C_AF"], C["C_AR"], C["M"], C["D_F"], C["D_R"], C["I_Z"]]
+        caf, car, mass, df, dr, iz = (float(c) for c in np.asarray(C, dtype=np.float64)[:6])
+        px, py, psi, vx, vy, r = (x[..., k] for k in range(6))
+        d = u[..., 1]
+        den = vx + 0.001                                  # nlp/dynamics.py:153
+        fyr = -car * (vy - dr * r) / den
+        fyf = -caf * ((vy + df * r) / den - d)
+        z = np.zeros_like(px)
+        f = np.stack([vx * np.cos(psi) - vy * np.sin(psi), vx * np.sin(psi) + vy * np.cos(psi), r,
+                      (-fyf * np.sin(d) + u[..., 0]) / mass + r * vy,
+                      (fyf * np.cos(d) + fyr) / mass - r * vx,
+                      (df * fyf * np.cos(d) - dr * fyr) / iz, x[..., 7], z, z], axis=-1)
+        # d(F_yf, F_yr)/d(vx, vy, r)
+        dfyf = [caf * (vy + df * r) / den ** 2, -caf / den, -caf * df / den]
+        dfyr = [car * (vy - dr * r) / den ** 2, -car / den, car * dr / den]
+        F[..., 0, 2] = -vx * np.sin(psi) - vy * np.cos(psi)
+        F[..., 0, 3] = np.cos(psi)
+        F[..., 0, 4] = -np.sin(psi)
+        F[..., 1, 2] = vx * np.cos(psi) - vy * np.sin(psi)
+        F[..., 1, 3] = np.sin(psi)
+        F[..., 1, 4] = np.cos(psi)
+        F[..., 2, 5] = 1.0
+        for k, c in enumerate((3, 4, 5)):
+            F[..., 3, c] = -np.sin(d) * dfyf[k] / mass
+            F[..., 4, c] = (np.cos(d) * dfyf[k] + dfyr[k]) / mass
+            F[..., 5, c] = (df * np.cos(d) * dfyf[k] - dr * dfyr[k]) / iz
+        F[..., 3, 4] += r
+        F[..., 3, 5] += vy
+        F[..., 4, 3] -= r
+        F[..., 4, 5] -= vx
+        F[..., 6, 7] = 1.0
     else:
         raise KeyError(f"oracle has no dynamics model {name!r}")
     return f, F

@@ -91,6 +91,9 @@ def load_reference():
         sys.modules.setdefault("gnss", ref.gnss)     # leastsquares.py's flat imports
         sys.modules.setdefault("utils", ref.gutils)
         ref.ls = _load("ref_leastsquares", f"{REF}/utils/leastsquares.py")
+        # utils/vehicle_sim.py: only get_parameters() is used (the car constants of
+        # autonomous-car.py:102); its module-level imports are the flat utils ones
+        ref.vehicle_sim = _load("ref_vehicle_sim", f"{REF}/utils/vehicle_sim.py")
     finally:
         sys.path.pop(0)
     return ref
@@ -183,6 +186,25 @@ def gen_plugins(ref):
     out["dyn_multi_receiver_x"] = xs
     out["dyn_multi_receiver_f"] = np.stack(fs)
     out["dyn_multi_receiver_F"] = np.stack(Fs)
+
+    # vehicle_dynamics_and_gnss (nlp/dynamics.py:148-174) with the car constants of
+    # autonomous-car.py:102 (utils/vehicle_sim.get_parameters); own generator so the
+    # streams of the cases above are unchanged.  vx = x[3] kept away from -0.001.
+    car = ref.vehicle_sim.get_parameters()
+    vr = np.random.default_rng(5678)
+    xs = vr.normal(size=(64, 9))
+    xs[:, 3] = 2.0 + 10.0 * np.abs(xs[:, 3])
+    us = vr.normal(size=(64, 2)) * np.array([2000.0, 0.2])
+    fs, Fs = [], []
+    for x, u in zip(xs, us):
+        f0, J = cstep_jac(lambda xx, uu: ref.dynamics.vehicle_dynamics_and_gnss(xx, uu, {"car_params": car}), x, u)
+        fs.append(f0); Fs.append(J)
+    out["dyn_vehicle_dynamics_and_gnss_x"] = xs
+    out["dyn_vehicle_dynamics_and_gnss_u"] = us
+    out["dyn_vehicle_dynamics_and_gnss_f"] = np.stack(fs)
+    out["dyn_vehicle_dynamics_and_gnss_F"] = np.stack(Fs)
+    out["dyn_vehicle_dynamics_and_gnss_par"] = np.array([car[k] for k in ("C_AF", "C_AR", "M", "D_F", "D_R", "I_Z")],
+                                                        dtype=np.float64)
 
     # measurements
     def meas(name, n, mk_params, jac=cstep_jac):
@@ -398,15 +420,15 @@ def gen_least_squares(ref):
     np.savez_compressed(os.path.join(OUT, "least_squares.npz"), **out)
 
 
-def main():
+def main(which=None):
     ref = load_reference()
-    gen_collocation(ref)
-    gen_plugins(ref)
-    gen_ekf(ref)
-    gen_gnss_io(ref)
-    gen_least_squares(ref)
+    gens = {"collocation": gen_collocation, "plugins": gen_plugins, "ekf": gen_ekf, "gnss_io": gen_gnss_io,
+            "least_squares": gen_least_squares}
+    for name, fn in gens.items():
+        if not which or name in which:
+            fn(ref)
     print("golden fixtures written to", OUT)
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1:])   # e.g. `gen_golden.py plugins` regenerates plugins.npz only

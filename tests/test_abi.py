@@ -68,3 +68,59 @@ def test_general_problem_dims_validation():
     d.meas_model, d.q, d.n_extra = 2, 3, 2             # extra variables need mixed rows
     d.dyn_model, d.n, d.m = 6, 5, 3
     assert lib.mhe_padded_dim(d) == -1
+
+
+def test_struct_size_guards_stale_bindings():
+    """ABI r02 (VERDICT weak #7): a binding that declares a truncated struct (the old
+    INTEGRATION.md stub stopped after T) is refused with MHE_ERR_DIMS before any later
+    field is read; so is one that omits struct_size (N lands in its place)."""
+    lib = _lib.load()
+
+    class Truncated(ctypes.Structure):   # struct_size .. T, nothing after
+        _fields_ = [f for f in _lib.MheDims._fields_ if f[0] != "dyn_cost"][:12]
+
+    assert Truncated._fields_[-1][0] == "T"
+    t = Truncated()
+    t.struct_size = ctypes.sizeof(t)
+    t.N, t.n, t.m, t.p, t.M, t.q, t.dyn_model, t.meas_model, t.T = 100, 2, 1, 2, 101, 0, 5, 1, 10.0
+    fn = lib.mhe_padded_dim
+    pd = ctypes.CFUNCTYPE(ctypes.c_int32, ctypes.POINTER(Truncated))(ctypes.cast(fn, ctypes.c_void_p).value)
+    assert pd(ctypes.byref(t)) == -1
+    cb = ctypes.CFUNCTYPE(ctypes.c_size_t, ctypes.POINTER(Truncated))(ctypes.cast(lib.mhe_const_bytes, ctypes.c_void_p).value)
+    assert cb(ctypes.byref(t)) == 0
+    # a solve entry point returns MHE_ERR_DIMS (no device pointer is touched)
+    sv = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.POINTER(Truncated), ctypes.c_void_p, ctypes.c_int32,
+                          *([ctypes.c_void_p] * 3), ctypes.c_int64, *([ctypes.c_void_p] * 2), ctypes.c_int64,
+                          *([ctypes.c_void_p] * 4), ctypes.c_int32, ctypes.c_double, ctypes.c_void_p)(
+        ctypes.cast(lib.mhe_gn_solve, ctypes.c_void_p).value)
+    assert sv(ctypes.byref(t), None, 1, None, None, None, 0, None, None, 0, None, None, None, None, 5, 1e-10, None) == -1
+
+    class NoSize(ctypes.Structure):      # the round-2 layout: N first
+        _fields_ = _lib.MheDims._fields_[1:]
+
+    o = NoSize()
+    o.N, o.n, o.m, o.p, o.M, o.q, o.dyn_model, o.meas_model, o.T = 100, 2, 1, 2, 101, 0, 5, 1, 10.0
+    pd2 = ctypes.CFUNCTYPE(ctypes.c_int32, ctypes.POINTER(NoSize))(ctypes.cast(fn, ctypes.c_void_p).value)
+    assert pd2(ctypes.byref(o)) == -1
+    # the full, current struct works
+    d = _lib.MheDims()
+    d.N, d.n, d.m, d.p, d.M, d.q, d.dyn_model, d.meas_model, d.T = 100, 2, 1, 2, 101, 0, 5, 1, 10.0
+    assert d.struct_size == ctypes.sizeof(_lib.MheDims) and lib.mhe_padded_dim(d) == 208
+    # EKF and least-squares structs: same guard
+    e = _lib.MheEkfDims()
+    e.struct_size -= 4
+    assert lib.mhe_ekf_run(e, 1, 1, None, None, None, 0, None, 0, None, 0, None, 0, None, None, 0, 0,
+                           None, None, None, None) == -1
+    ls = _lib.MheLsDims()
+    ls.struct_size = 0
+    assert lib.mhe_ls_run(ls, 1, 1, *([None] * 13)) == -1
+
+
+def test_integration_stub_declares_the_full_struct():
+    """INTEGRATION.md's ctypes stub must declare mhe_dims exactly as the library does."""
+    import re as _re
+    text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    m = _re.search(r"class mhe_dims\(ctypes.Structure\):.*?_fields_ = \[(.*?)\]\n", text, _re.S)
+    assert m, "INTEGRATION.md has no mhe_dims stub"
+    names = _re.findall(r'\("([a-z_A-Z]+)"', m.group(1))
+    assert names == [f[0] for f in _lib.MheDims._fields_]

@@ -112,6 +112,33 @@ def test_bounds_iterates_match_oracle_fixed_count_large_system_path():
     assert np.allclose(cost, cr, rtol=1e-10)
 
 
+def _backtracking_case():
+    """A far start (2 X_init + 2) under the same bounds: the oracle's Armijo search
+    halves the step several times (the line search must use the gradient
+    at the iterate, not the forward-substituted right-hand side)."""
+    w, bounds, pb = _bounds_case()
+    X0 = 2.0 * w.X_init + 2.0
+    trace = []
+    Xr, cr, ir, sr = gn.gauss_newton(pb, X0, _U(w), w.Y, max_iter=8, tol=0.0, trace=trace)
+    assert sum(a < 1.0 for _, _, a in trace) >= 4, "the case should backtrack"
+    return w, bounds, pb, X0, (Xr, cr, ir, sr)
+
+
+@pytest.mark.parametrize("force_large", [False, True])
+def test_bounds_line_search_backtracking_matches_oracle(force_large):
+    """Same accept / backtrack decisions as the oracle: iterates after 8 steps (tol 0)
+    with several halvings, on the register-resident and the large-system path."""
+    w, bounds, pb, X0, (Xr, cr, ir, sr) = _backtracking_case()
+    s = solver.from_workload(w, bounds=bounds, force_large=force_large)
+    assert s.large_system == force_large
+    X, cost, iters, status = _np(s.solve(X0, w.U, w.Y, max_iter=8, tol=0.0))
+    err = np.abs(X - Xr).max()
+    print(f"backtracking case (force_large={force_large}): max |X - X_oracle| = {err:.3e}")
+    assert iters.tolist() == ir.tolist() == [8] * w.B and status.tolist() == sr.tolist()
+    assert err <= 1e-9 * (1 + np.abs(Xr).max())
+    assert np.allclose(cost, cr, rtol=1e-10)
+
+
 def test_huber_on_large_system_path_is_refused():
     w = configs.make_c2(B=2, N=150)
     s = solver.from_workload(w, dyn_cost="huber", huber_delta=DELTA)

@@ -80,6 +80,16 @@ def test_oracle_dynamics_vs_reference(golden, name):
     assert np.allclose(F, g[f"dyn_{name}_F"], rtol=1e-13, atol=1e-13)
 
 
+def test_oracle_vehicle_dynamics_and_gnss_vs_reference(golden):
+    """nlp/dynamics.py:148-174 with the reference car constants (params["car_params"]),
+    values and complex-step Jacobians of the reference plug-in."""
+    g = golden["plugins"]
+    name = "vehicle_dynamics_and_gnss"
+    f, F = om.dyn_eval(name, g[f"dyn_{name}_x"], g[f"dyn_{name}_u"], g[f"dyn_{name}_par"])
+    assert np.allclose(f, g[f"dyn_{name}_f"], rtol=1e-13, atol=1e-12)
+    assert np.allclose(F, g[f"dyn_{name}_F"], rtol=1e-12, atol=1e-12)
+
+
 def test_oracle_multi_receiver_m0(golden):
     g = golden["plugins"]
     f, F = om.dyn_eval("multi_receiver", g["dyn_multi_receiver_x"], None)
