@@ -58,7 +58,7 @@ __host__ __device__ inline BigConst big_const_layout(int P, int M, int n, int p,
 }
 
 struct BigWs {  // per-trajectory workspace offsets in doubles
-  size_t H, LT, BV, YV, XE, GEe, Ge, Es, FtE, Vs, FtV, GZe, HZZe, GZVe, BM, ZM, DZ, ACT, GV, NZ, total;
+  size_t H, LT, BV, YV, XE, GEe, Ge, Es, FtE, Vs, FtV, GZe, HZZe, GZVe, BM, ZM, DZ, ACT, GV, NZ, LAM, total;
 };
 
 // nz extra variables, nc equality constraints (border of the KKT system)
@@ -91,6 +91,7 @@ __host__ __device__ inline BigWs big_ws_layout(int P, int M, int n, int NT, int 
   W.GV = o;   o = al(o + (size_t)dp);                            // bounds: -g at the iterate (k_big_chol
                                                                  // overwrites BV with the forward solve)
   W.NZ = o;   o = al(o + 1);                                     // bounds: the cost's rounding level at X
+  W.LAM = o;  o = al(o + (size_t)P * n);                         // Huber IRLS weights c_k lambda_ka
   W.total = o;
   return W;
 }
@@ -127,6 +128,8 @@ struct BigArgs {
   double dpar[8];    // mhe_dims.dyn_par (dynamics plug-in params)
   const double* Rw;  // per-solve measurement weights (B|1, M, p, p) or NULL = the constants' Rw
   long long rwstride;
+  int huber;         // MHE_COST_HUBER: IRLS weights (k_big_resid), D^T diag(c lambda) D blocks (k_big_assemble)
+  double huber_delta;
 };
 
 // measurement weights of trajectory b: the per-solve array when given, else the constants'
@@ -250,31 +253,44 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_resid(BigArgs a, int final
     double W[n], V[n];
     for (int c = 0; c < n; ++c) W[c] = a.alpha * dx[c] - f[c];
     const double ck = cw[k];
-    for (int r = 0; r < n; ++r) {
-      double s = 0.0;
-      for (int c = 0; c < n; ++c) s += Qw[r * n + c] * W[c];
-      V[r] = ck * s;
-      cost += W[r] * V[r];
+    double* Ek = ws + WL.Es + (size_t)k * n * n;
+    if (a.huber) {
+      // pseudo_huber_loss (cost_functions.py:25-31) by IRLS, as k_gn: lambda = c q / sqrt(1 +
+      // W^2 / delta^2) per component (only diag(Qw) enters), V = lambda W, E = diag(lambda) F
+      const double dl = a.huber_delta;
+      for (int r = 0; r < n; ++r) {
+        const double q = Qw[r * n + r];
+        const double sr = sqrt(1.0 + W[r] * W[r] / (dl * dl));
+        const double lam = ck * (q / sr);
+        V[r] = lam * W[r];
+        cost += ck * (2.0 * q * dl * dl * (sr - 1.0));
+        ws[WL.LAM + k * n + r] = lam;
+        for (int c = 0; c < n; ++c) Ek[r * n + c] = lam * F[r * n + c];
+      }
+    } else {
+      for (int r = 0; r < n; ++r) {
+        double s = 0.0;
+        for (int c = 0; c < n; ++c) s += Qw[r * n + c] * W[c];
+        V[r] = ck * s;
+        cost += W[r] * V[r];
+        for (int c = 0; c < n; ++c) {
+          double e = 0.0;
+          for (int t = 0; t < n; ++t) e += Qw[r * n + t] * F[t * n + c];
+          Ek[r * n + c] = ck * e;
+        }
+      }
     }
     for (int r = 0; r < n; ++r) {
       ws[WL.Vs + k * n + r] = V[r];
       double s = 0.0;
       for (int t = 0; t < n; ++t) s += F[t * n + r] * V[t];
       ws[WL.FtV + k * n + r] = s;
-      for (int c = 0; c < n; ++c) {
-        double e = 0.0;
-        for (int t = 0; t < n; ++t) e += Qw[r * n + t] * F[t * n + c];
-        ws[WL.Es + (k * n + r) * n + c] = ck * e;
-      }
     }
+    // F^T E (E read back from this thread's own writes)
     for (int r = 0; r < n; ++r)
       for (int c = 0; c < n; ++c) {
         double u = 0.0;
-        for (int t = 0; t < n; ++t) {
-          double e = 0.0;
-          for (int s2 = 0; s2 < n; ++s2) e += Qw[t * n + s2] * F[s2 * n + c];
-          u += F[t * n + r] * ck * e;
-        }
+        for (int t = 0; t < n; ++t) u += F[t * n + r] * Ek[t * n + c];
         ws[WL.FtE + (k * n + r) * n + c] = u;
       }
   }
@@ -549,11 +565,31 @@ __global__ __launch_bounds__(256, 4) void k_big_assemble(BigArgs a) {
         if (q < np) acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0 * g0[q], b0, acc[q], 0, 0, 0);
     }
   }
+  if (a.huber) {
+    // pseudo-Huber IRLS: the dynamics part a^2 (D^T C D) (x) Qw is no longer constant --
+    // block (ca, ca) gets a^2 D^T diag(c lambda_ca) D (k_big_resid's weights), a GEMM
+    // over the P nodes with the same operand layout as the epoch contraction
+    const double* LAM = ws + WL.LAM;
+    const double a2 = a.alpha * a.alpha;
+    int lo[BIG_PCH];  // lambda offset of a diagonal pair, -1 otherwise
+#pragma unroll
+    for (int q = 0; q < BIG_PCH; ++q) lo[q] = (q < np && a.pa[q0 + q] == a.pb[q0 + q]) ? a.pa[q0 + q] : -1;
+#pragma unroll 1
+    for (int k0 = 0; k0 < P; k0 += 4) {
+      const int k = k0 + (lane >> 4);
+      const int kc = k < P ? k : P - 1;
+      const double dv = (k < P && vr) ? D[(size_t)kc * P + row] : 0.0;
+      const double ev = (k < P && vc) ? D[(size_t)kc * P + col] : 0.0;
+#pragma unroll
+      for (int q = 0; q < BIG_PCH; ++q)
+        if (lo[q] >= 0) acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(dv * (a2 * LAM[kc * n + lo[q]]), ev, acc[q], 0, 0, 0);
+    }
+  }
 #pragma unroll
   for (int q = 0; q < BIG_PCH; ++q) {
     if (q < np) {
       const int ca = a.pa[q0 + q], cb = a.pb[q0 + q];
-      const double qab = a.alpha * a.alpha * Qw[ca * n + cb];
+      const double qab = a.huber ? 0.0 : a.alpha * a.alpha * Qw[ca * n + cb];
       // tile (it, jt) of block (ca, cb) and, off the diagonal pair, its transpose into (jt, it)
 #pragma unroll
       for (int tp = 0; tp < 2; ++tp) {
@@ -1111,6 +1147,11 @@ __device__ double big_cost(const BigArgs& a, const double* X, int b, double* red
     for (int c = 0; c < n; ++c) W[c] = a.alpha * dx[c] - f[c];
     const double ck = cw[k];
     for (int r = 0; r < n; ++r) {
+      if (a.huber) {  // pseudo_huber_loss (cost_functions.py:25-31), as k_big_resid
+        const double q = Qw[r * n + r], dl = a.huber_delta;
+        cost += ck * (2.0 * q * dl * dl * (sqrt(1.0 + W[r] * W[r] / (dl * dl)) - 1.0));
+        continue;
+      }
       double s = 0.0;
       for (int c = 0; c < n; ++c) s += Qw[r * n + c] * W[c];
       cost += W[r] * (ck * s);

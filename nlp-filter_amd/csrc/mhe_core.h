@@ -1897,17 +1897,24 @@ inline bool meas_info(int id, int n, int& p, int& q, bool& linear) {
 // the large-system path so both paths can be compared on identical inputs.
 // Mixed-row problems, extra variables and equality constraints
 // always take the large-system path (it carries the bordered KKT step).
-inline bool is_big(const mhe_dims* dm) {
-  if (dm->force_large) return true;
-  if (dm->meas_model == MHE_MEAS_MIXED || dm->n_extra > 0 || dm->n_eq > 0) return true;
-  return ((dm->N + 1) * dm->n + 15) / 16 > MAX_NT;
-}
-
 inline int smem_bytes(const mhe_dims* dm, int NT, bool bounded = false) {
   int p, q;
   bool lin;
   meas_info(dm->meas_model, dm->n, p, q, lin);
   return smem_layout(dm->N + 1, dm->M, dm->n, NT, !lin, bounded).total * (int)sizeof(double);
+}
+
+// The register-resident kernel keeps per-row measurement blocks G_i (n x n) in LDS;
+// when they do not fit (e.g. autonomous-car.py: 231 rows x 9 x 9) the problem takes
+// the large-system path, which groups rows by epoch.
+constexpr int REG_LDS_LIMIT = 160 * 1024;
+
+inline bool is_big(const mhe_dims* dm) {
+  if (dm->force_large) return true;
+  if (dm->meas_model == MHE_MEAS_MIXED || dm->n_extra > 0 || dm->n_eq > 0) return true;
+  const int NT = ((dm->N + 1) * dm->n + 15) / 16;
+  if (NT > MAX_NT) return true;
+  return smem_bytes(dm, NT, true) > REG_LDS_LIMIT;
 }
 
 inline size_t big_ws_doubles(const mhe_dims* dm, int NT) {
@@ -1935,7 +1942,7 @@ int launch_gn(const mhe_dims* dm, GnArgs& a, int batch, int mode, hipStream_t st
     const bool bounded = mode == MODE_SOLVE && dm->n_bounds > 0;
     int smem = smem_bytes(dm, a.NT, bounded);
     if (const char* pad = getenv("MHE_DEBUG_SMEM_PAD")) smem += atoi(pad);  // debug: force occupancy
-    if (smem > 160 * 1024) return MHE_ERR_UNSUPPORTED;
+    if (smem > REG_LDS_LIMIT) return MHE_ERR_UNSUPPORTED;
     void (*kern)(GnArgs) = nullptr;
     const bool huber = dm->dyn_cost == MHE_COST_HUBER;
     if (bounded) kern = huber ? k_gn_bounded<DYN, MEAS, MAX_SLOTS, true> : k_gn_bounded<DYN, MEAS, MAX_SLOTS>;

@@ -385,7 +385,6 @@ int mhe_solve(const mhe_dims* dims, const void* const_buf, const mhe_solve_args*
   if (!ops) return MHE_ERR_UNSUPPORTED;
   hipStream_t st = (hipStream_t)stream;
   if (is_big(dims)) {
-    if (dims->dyn_cost != MHE_COST_L2) return MHE_ERR_UNSUPPORTED;  // Huber: fused path only (this build)
     if (!g->workspace || g->workspace_bytes < mhe_workspace_bytes(dims, batch)) return MHE_ERR_NULL;
     BigArgs A = {};
     A.cbuf = (const char*)const_buf;
@@ -407,6 +406,8 @@ int mhe_solve(const mhe_dims* dims, const void* const_buf, const mhe_solve_args*
     A.nz = dims->n_extra;
     A.nc = dims->n_eq;
     A.Z = g->Z_out;
+    A.huber = dims->dyn_cost == MHE_COST_HUBER;
+    A.huber_delta = dims->huber_delta;
     A.tag = const_tag(dims, NT);
     if (A.X != g->X0 &&
         hipMemcpyAsync(A.X, g->X0, sizeof(double) * batch * A.P * A.n, hipMemcpyDeviceToDevice, st) != hipSuccess)

@@ -224,14 +224,25 @@ def normal_equations_explicit(pb, X, U, Y, PAR=None, x0=None):
     return np.stack(Hs), np.stack(gs), np.array(cs)
 
 
-def gauss_newton(pb, X0, U, Y, PAR=None, x0=None, max_iter=20, tol=1e-10, trace=None):
+def perturb_rel(A, seed):
+    """A with every entry moved by eps |A_ij| (random sign; symmetric for square A):
+    the backward error of ANY evaluation order of A's sums (tests/tolerance.py)."""
+    rng = np.random.default_rng(seed)
+    S = rng.choice([-1.0, 1.0], size=A.shape)
+    if A.ndim >= 2 and A.shape[-1] == A.shape[-2]:
+        S = np.triu(S) + np.swapaxes(np.triu(S, 1), -1, -2)
+    return A * (1.0 + np.finfo(np.float64).eps * S)
+
+
+def gauss_newton(pb, X0, U, Y, PAR=None, x0=None, max_iter=20, tol=1e-10, trace=None, perturb=None):
     """Batched GN with the same stopping rule as the HIP kernel.
 
     Per trajectory: solve H delta = -g (Cholesky), X += delta, iters += 1;
     converged when max|delta| <= tol * (1 + max|X|). Converged trajectories are
     frozen. Returns X, cost (at the returned X), iters, status.
     With bounds (pb.lb / pb.ub) the iteration is the projected Newton method of
-    ``gauss_newton_bounded``.
+    ``gauss_newton_bounded``.  ``perturb`` (a seed) moves every entry of H and g by
+    eps of its magnitude each iteration -- the conditioning floor of tests/tolerance.py.
     """
     if pb.lb is not None or pb.ub is not None:
         return gauss_newton_bounded(pb, X0, U, Y, PAR, x0, max_iter, tol, trace)
@@ -249,6 +260,8 @@ def gauss_newton(pb, X0, U, Y, PAR=None, x0=None, max_iter=20, tol=1e-10, trace=
         if pb.Rw.ndim == 4:
             pbs = _with_rw(pb, pb.Rw[idx])
         H, g, _ = normal_equations(pbs, X[idx], sub(U), Y[idx], sub(PAR), sub(x0))
+        if perturb is not None:  # rounding-level perturbation of the normal equations
+            H, g = perturb_rel(H, perturb), perturb_rel(g, perturb + 1)
         for t, b in enumerate(idx):
             try:
                 L = np.linalg.cholesky(H[t])

@@ -173,8 +173,10 @@ def kkt_step(H, g, C, cval):
     return step, sol[Hf.shape[0]:]
 
 
-def gauss_newton_general(pb, X0, Z0, U, Y, PAR, x0=None, max_iter=20, tol=1e-10):
-    """Returns X, Z, cost, iters, status (same stopping rule / status codes as the kernels)."""
+def gauss_newton_general(pb, X0, Z0, U, Y, PAR, x0=None, max_iter=20, tol=1e-10, perturb=None):
+    """Returns X, Z, cost, iters, status (same stopping rule / status codes as the kernels).
+    ``perturb`` (a seed): H and g moved by eps of every entry's magnitude each iteration
+    (gn.perturb_rel -- the conditioning floor of tests/tolerance.py)."""
     X = np.array(X0, dtype=np.float64, copy=True)
     B, P, n = X.shape
     nz = pb.n_extra
@@ -194,6 +196,8 @@ def gauss_newton_general(pb, X0, Z0, U, Y, PAR, x0=None, max_iter=20, tol=1e-10)
             Ub = None if U is None else U[min(b, U.shape[0] - 1)][None]
             H, g, _ = normal_equations_full(pbb, X[sl], Z[sl], Ub, Y[sl], PAR[min(b, PAR.shape[0] - 1)][None],
                                             None if x0 is None else x0[sl])
+            if perturb is not None:
+                H, g = gn.perturb_rel(H, perturb), gn.perturb_rel(g, perturb + 1)
             v = np.concatenate([X[b].ravel(), Z[b]])
             cval = C @ v
             try:

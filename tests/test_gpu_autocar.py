@@ -6,7 +6,7 @@ against the same script on the oracle (tests/autocar.py).
 The reference's stored IPOPT results for this script (nlp-l2.pkl / nlp-huber.pkl) and
 its inputs are Python-2 pickles that the permitted safe loader refuses (DESIGN.md
 §8), so the inputs are seeded synthetic data of the same shape and the oracle is the
-checker.  Tolerance (tests/tolerance.py): 32 floor + 1e-8 (1 + max|X|), floor = the
+checker.  Tolerance (tests/tolerance.py): 8 floor + 1e-8 (1 + max|X|), floor = the
 oracle loop's own change when every pseudorange moves by eps |y| (both sides stop at
 max|s| <= 1e-10 (1 + max|X|), so converged iterates agree to ~tol, not to rounding).
 """

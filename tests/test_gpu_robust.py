@@ -14,7 +14,7 @@ torch = pytest.importorskip("torch")
 
 pytestmark = pytest.mark.gpu
 
-from mhe import _lib, configs, solver  # noqa: E402
+from mhe import configs, solver  # noqa: E402
 from oracle import gn  # noqa: E402
 
 DELTA = 0.02
@@ -139,11 +139,33 @@ def test_bounds_line_search_backtracking_matches_oracle(force_large):
     assert np.allclose(cost, cr, rtol=1e-10)
 
 
-def test_huber_on_large_system_path_is_refused():
-    w = configs.make_c2(B=2, N=150)
+@pytest.mark.parametrize("max_iter,tol", [(5, 0.0), (400, 1e-10)])
+def test_huber_large_system_path_matches_oracle(max_iter, tol):
+    """pseudo-Huber on the large-system path (d = 302 > 208 by size):
+    IRLS weights in k_big_resid, a^2 D^T diag(c lambda) D blocks in k_big_assemble."""
+    w = configs.make_c2(B=3, N=150)
     s = solver.from_workload(w, dyn_cost="huber", huber_delta=DELTA)
-    with pytest.raises(_lib.MheCallError):
-        s.solve(w.X_init, w.U, w.Y, max_iter=2)
+    assert s.large_system
+    X, cost, iters, status = _np(s.solve(w.X_init, w.U, w.Y, max_iter=max_iter, tol=tol))
+    Xr, cr, ir, sr = gn.gauss_newton(_pb(w, dyn_cost="huber", delta=DELTA), w.X_init, _U(w), w.Y,
+                                     max_iter=max_iter, tol=tol)
+    assert status.tolist() == sr.tolist()
+    assert np.all(np.abs(iters - ir) <= (0 if tol == 0 else 1))
+    lim = 1e-10 if tol == 0 else 1e-8
+    err = np.abs(X - Xr).max()
+    print(f"huber large path ({max_iter}, {tol}): max err {err:.3e}")
+    assert err <= lim * (1 + np.abs(Xr).max())
+    assert np.allclose(cost, cr, rtol=lim)
+
+
+def test_huber_large_and_register_paths_agree():
+    w = configs.make_c2(B=4, N=20)
+    sr_ = solver.from_workload(w, dyn_cost="huber", huber_delta=DELTA)
+    sb = solver.from_workload(w, dyn_cost="huber", huber_delta=DELTA, force_large=True)
+    a = _np(sr_.solve(w.X_init, w.U, w.Y, max_iter=6, tol=0.0))
+    b = _np(sb.solve(w.X_init, w.U, w.Y, max_iter=6, tol=0.0))
+    assert np.abs(a[0] - b[0]).max() <= 1e-10 * (1 + np.abs(a[0]).max())
+    assert np.allclose(a[1], b[1], rtol=1e-10)
 
 
 def test_facade_huber_and_bounds_match_oracle():

@@ -10,14 +10,22 @@ and B with per-window parameters and R = 0 slots), zA = zB at every node
   velocities from the reference's runLeastSquares).  Tolerance: states at t = T
   and t = DT within 1e-6 * (1 + max|x|) (x holds clock biases ~3e4 m; the
   pseudorange rows lose log10(|y| / |y - h|) ~ 5 digits to cancellation).
-* Consistency with the reference's stored IPOPT results (NLP_{A,B}.csv), read in
-  place when /root/reference is present: the oracle replica on the real logs.
-  PARITY UNPINNED for this case: IPOPT is absent here, our Gauss-Newton optimum is
-  unique (multi-start) and KKT-stationary, yet the stored fixes differ by
-  1.5-4 m (B) and 2-31 m (A, whose ~-186 m/s clock drift the model's prior on the
-  drift rate cannot follow: A's pseudorange residuals reach 500 m).  The check
-  below only guards the script semantics (e.g. using all 12 slots instead of
-  N_sat = 10 moves every fix by ~900 m).
+* Against the reference's stored results, read in place when /root/reference is
+  present (build container):
+  - the least-squares fixes the script feeds the NLP (controls, first prior) match
+    the stored LS_{A,B}.csv to 1e-7 m -- the data pipeline is the reference's;
+  - the stored IPOPT fixes NLP_{A,B}.csv are not the optimum of the objective the
+    script builds: with A's and B's horizontal positions held at the stored values
+    and everything else re-minimised, the objective sits 586 above the unique optimum
+    that the oracle and the GPU reach in window 0 (identical inputs and prior on both
+    sides; J* = 1.1e6 -- receiver A's ~400 m pseudorange misfit dominates), and the
+    objective's gradient on the held coordinates is ~190 per metre there, so no
+    stationary point has those positions.  At a point converged to IPOPT's tol the excess would be second
+    order in the ~1e-8 scaled dual infeasibility; 5e-4 of J is what termination away
+    from stationarity leaves (CasADi's Opti accepts IPOPT's "Solved To Acceptable
+    Level", whose default acceptable_dual_inf_tol is 1e10).  Named cause of the
+    4 m (A) / 3.5 m (B) window-0 difference; later windows inherit different priors.
+    tools/diag_multirx.py prints the per-window table (profiles/r03_multirx_gap.txt).
 """
 import os
 
@@ -59,8 +67,7 @@ def test_two_receiver_mhe_facade_matches_oracle(golden):
     assert np.abs(XT[:, 2] - XT[:, 7]).max() <= 1e-9 * scale   # zA = zB holds (every node, so at t = T)
 
 
-@pytest.mark.skipif(not os.path.isdir(REF_DATA), reason="reference data not present (GPU box)")
-def test_oracle_replica_consistent_with_stored_ipopt_results():
+def _ref_inputs():
     from oracle import leastsquares as ols
     from utils import data as gd, utils as gu
     dA = gd.load_gnss_logs(REF_DATA + "/rec1/rec1_gnss_log_50y_moving_")
@@ -69,21 +76,35 @@ def test_oracle_replica_consistent_with_stored_ipopt_results():
     tA, tB = np.asarray(dA["t"], float), np.asarray(dB["t"], float)
     t0 = min(tA.min(), tB.min())
     dA["t"], dB["t"] = tA - t0, tB - t0
-    x = np.zeros(3)
+    x = np.zeros(3)   # the reference's shared mutable default warm start (utils/leastsquares.py:19)
+    outs = {}
+    for tag, d in (("A", dA), ("B", dB)):
+        outs[tag] = ols.run_least_squares(d["sat_pos"], d["pr"], d["sat_vel"], d["pr_rate"], x=x)
+    return dA, dB, p_ref, outs
 
-    def ls(d):
-        o = ols.run_least_squares(d["sat_pos"], d["pr"], d["sat_vel"], d["pr_rate"], x=x)
-        e = np.array([gu.ecef2enu(p, p_ref) for p in o["x"]])
-        v = np.array([gu.ecef2enu(q, p_ref, rotation_only=True) for q in o["v"]])
-        return {"x_ENU": e[:, 0], "y_ENU": e[:, 1], "z_ENU": e[:, 2], "bias": o["b"],
-                "xd_ENU": v[:, 0], "yd_ENU": v[:, 1], "zd_ENU": v[:, 2]}
 
-    lsA, lsB = ls(dA), ls(dB)
-    nw = 8
-    XT, _, st = two_rx_mhe_oracle(dA, dB, lsA, lsB, p_ref, nw, lambda s: gu.ecef2enu(s, p_ref))
-    assert (st == 0).all()
-    for sl, f, lim in ((slice(0, 3), "NLP_A.csv", 40.0), (slice(5, 8), "NLP_B.csv", 6.0)):
-        ll = np.array([gu.ecef2lla(gu.enu2ecef(p, p_ref))[:2] for p in XT[:, sl]])
-        ref = np.loadtxt(f"{REF_DATA}/{f}", delimiter=",")[:nw]
-        err_m = np.abs(ll - ref).max(axis=1) * 1.11e5
-        assert err_m.max() < lim, (f, err_m)
+@pytest.mark.skipif(not os.path.isdir(REF_DATA), reason="reference data not present (GPU box)")
+def test_least_squares_inputs_match_stored_ls_csv():
+    from utils import utils as gu
+    _, _, _, outs = _ref_inputs()
+    for tag in ("A", "B"):
+        lla = np.array([gu.ecef2lla(p) for p in outs[tag]["x"]])[:, :2]
+        ref = np.loadtxt(f"{REF_DATA}/LS_{tag}.csv", delimiter=",")
+        err_m = np.abs(lla - ref).max() * 1.11e5
+        print(f"LS_{tag}: max {err_m:.2e} m over {len(ref)} epochs")
+        assert lla.shape == ref.shape and err_m < 1e-7
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_DATA), reason="reference data not present (GPU box)")
+def test_stored_ipopt_fixes_are_not_stationary_for_the_script_objective():
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import diag_multirx
+    line = diag_multirx.main(1)[0]
+    js, jc = (float(v) for v in (line.split("J* = ")[1].split(" ")[0], line.split("J_c = ")[1].split(" ")[0]))
+    gap = jc - js
+    print(line)
+    assert "(status 0)" in line and "J_c" in line
+    # the unique optimum (oracle) is lower than anything consistent with the stored fixes by far
+    # more than rounding (~1e-9 J) or a tol-converged interior-point solve could leave
+    assert gap > 1e-5 * js, gap

@@ -1,26 +1,30 @@
 """Parity tolerances derived from the problem.
 
-Two correct fp64 evaluations of the same Gauss-Newton iteration differ for two reasons:
+Two correct fp64 evaluations of the same Gauss-Newton iteration differ for two reasons,
+and both are MEASURED on the oracle, not assumed:
 
  (1) rounding of the residual y - h(x).  Pseudoranges (|y| ~ 2.2e7 m) carry eps |y|
      ~ 5e-9 m of rounding in ANY evaluation order (h is a sqrt of squares of ~2e7 m
-     differences).  Its effect on the result is MEASURED, not assumed: the oracle is
-     re-run with every y moved by eps |y| (random sign) and the largest change of
-     the result is the floor.
- (2) summation order in the normal equations and the factorisation: relative,
-     REL (1 + max|X|) for iterates, SURVEY.md §8(c) (1e-10).
+     differences): floor_y = the change of the oracle's result when every y moves by
+     eps |y| (random sign);
+ (2) the summation order of the normal equations and the factorisation: floor_H = the
+     change when every entry of H and g moves by eps of its magnitude, every iteration
+     (oracle ``perturb``) -- a backward-stable solver's error, amplified by cond(H).
 
-    bound = FLOOR_MULT * floor + REL * (1 + max|X|)
+    bound = FLOOR_MULT * max(floor_y, floor_H) + REL * (1 + max|X|)      (REL: SURVEY §8(c))
 
-For a pseudorange problem the floor is ~1e-8 m, so the bound is ~1e-6 m and a
-1e-4 m error fails (the round-2 bound 1e-9 kappa (1 + max|X|) let ~2 m through).
-Every test prints the observed error beside its bound.
+For C2 / C3 shapes the floors are ~1e-15 / ~1e-9 m, so a 1e-4 m error fails (the round-2
+bound 1e-9 kappa (1 + max|X|) let ~2 m through).  The C4 shape (N = 500) is the
+exception: its normal equations are so ill-conditioned that moving H by eps moves X by
+~1 mm -- no evaluation order resolves better, and the bound says so.  Every test prints
+the observed error beside its bound.
 """
 import numpy as np
 
-FLOOR_MULT = 32.0
+FLOOR_MULT = 8.0
 REL = 1e-10
 EPS = np.finfo(np.float64).eps
+SEED_H = 5
 
 
 def perturbed(Y, seed=12345):
@@ -29,11 +33,14 @@ def perturbed(Y, seed=12345):
     return Y * (1.0 + EPS * rng.choice([-1.0, 1.0], size=np.shape(Y)))
 
 
-def floor(run, Y, seed=12345):
-    """max |run(Y') - run(Y)| over the outputs of ``run`` (a tuple of arrays), Y' =
-    perturbed(Y): the change any evaluation order may legitimately produce."""
-    a, b = run(Y), run(perturbed(Y, seed))
-    return [float(np.abs(np.asarray(x) - np.asarray(y)).max()) for x, y in zip(a, b)]
+def floor(run, Y, seed=12345, conditioning=True):
+    """Per output of ``run(Y, perturb)`` (a tuple of arrays; perturb = None or a seed for
+    the oracle's rounding-level perturbation of H and g): max(floor_y, floor_H)."""
+    a = run(Y, None)
+    b = run(perturbed(Y, seed), None)
+    c = run(Y, SEED_H) if conditioning else a
+    return [float(max(np.abs(np.asarray(x) - np.asarray(y)).max(), np.abs(np.asarray(x) - np.asarray(z)).max()))
+            for x, y, z in zip(a, b, c)]
 
 
 def bound(fl, X, rel=REL):
