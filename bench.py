@@ -11,8 +11,10 @@ GN_ITERS full Gauss-Newton iterations per trajectory (tol = 0): residual +
 Jacobian, J^T W J / J^T W r assembly, register-tiled Cholesky, two triangular
 solves, update.  value = (all ranks) B * P * GN_ITERS * K / max-rank wall.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu]
-N > 1 is launched by torch.distributed.run (RANK/LOCAL_RANK/WORLD_SIZE env).
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu] [--global-batch G]
+N > 1 is launched by torch.distributed.run (RANK/LOCAL_RANK/WORLD_SIZE env).  Default:
+weak scaling (1024 trajectories per GPU); --global-batch 1024 splits one fixed batch
+over the ranks (strong scaling, "scaling": "strong").
 """
 import argparse
 import json
@@ -82,34 +84,38 @@ def cpu_baseline(w, iters, sample_B, target_s=10.0):
             X = port.iteration(X, U[ix], w.Y[ix])
         return X
 
-    reps = 0
+    # the median of >= 5 repetitions after a warm-up, each repetition one
+    # pass of `iters` GN iterations over the sample, repeated until ~target_s of wall
+    reps = []
     with threadpool_limits(1), ThreadPoolExecutor(max_workers=cores) as ex:
         work(chunks[0][:2])  # warm-up
         t0 = time.perf_counter()
-        while True:
+        while len(reps) < 5 or time.perf_counter() - t0 < target_s:
+            t1 = time.perf_counter()
             list(ex.map(work, chunks))
-            reps += 1
-            dt = time.perf_counter() - t0
-            if dt >= target_s:
-                break
-    # SURVEY.md 8(d) also asks for the 1-core figure: a 64-trajectory slice, ~3 s
+            reps.append(time.perf_counter() - t1)
+    dt = time.perf_counter() - t0
+    med = float(np.median(reps))
+    # the 1-core figure: a 64-trajectory slice, ~target_s / 3
     one = np.arange(min(64, B))
+    reps1 = []
     with threadpool_limits(1):
         work(one[:2])
-        t1, reps1 = time.perf_counter(), 0
-        while True:
+        t0 = time.perf_counter()
+        while len(reps1) < 5 or time.perf_counter() - t0 < target_s / 3:
+            t1 = time.perf_counter()
             work(one)
-            reps1 += 1
-            dt1 = time.perf_counter() - t1
-            if dt1 >= target_s / 3:
-                break
-    return {"value": reps * B * w.P * iters / dt, "unit": "GN collocation-point updates/s", "cores": cores,
+            reps1.append(time.perf_counter() - t1)
+    med1 = float(np.median(reps1))
+    return {"value": B * w.P * iters / med, "unit": "GN collocation-point updates/s", "cores": cores,
             "kind": "port",
-            "value_1core": reps1 * len(one) * w.P * iters / dt1,
-            "sample": f"{reps} x ({B} of the {w.B} C2 trajectories x {iters} GN iterations) with oracle.gn.CpuPort "
-                      f"(same algorithm: constant J^T W J part precomputed, LAPACK dpotrf + 2 trsv per trajectory), "
-                      f"{cores} worker threads, {dt:.1f} s wall; value_1core: {reps1} x {len(one)} trajectories "
-                      f"x {iters} iterations on one thread, {dt1:.1f} s"}
+            "value_1core": len(one) * w.P * iters / med1,
+            "statistic": "median over repetitions",
+            "sample": f"median of {len(reps)} repetitions ({dt:.1f} s wall) of ({B} of the {w.B} C2 trajectories x "
+                      f"{iters} GN iterations) with oracle.gn.CpuPort (same algorithm: constant J^T W J part "
+                      f"precomputed, LAPACK dpotrf + 2 trsv per trajectory), {cores} worker threads; value_1core: "
+                      f"median of {len(reps1)} repetitions of {len(one)} trajectories x {iters} iterations on one "
+                      f"thread"}
 
 
 def main():
@@ -117,7 +123,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=1024, help="trajectories per GPU")
+    ap.add_argument("--batch", type=int, default=1024, help="trajectories per GPU (weak scaling)")
+    ap.add_argument("--global-batch", type=int, default=None,
+                    help="strong scaling: this many trajectories in total, split over the ranks "
+                         "(dist.shard_range); the north star's fixed batch-1024 at 1/2/4/8 GPUs")
     ap.add_argument("--iters", type=int, default=GN_ITERS)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=1024)
@@ -135,12 +144,20 @@ def main():
     torch.cuda.set_device(dev)
     dist.init("nccl", dev)
 
-    w = configs.make_c2(B=args.batch, seed=dist.shard_seed(1, rank))
+    if args.global_batch:
+        # strong scaling: one global problem set (seed 1), rank r solves its contiguous shard
+        lo, hi = dist.shard_range(args.global_batch, world, rank)
+        w = configs.make_c2(B=args.global_batch, seed=1)
+        for k in ("X_init", "Y", "X_true"):
+            setattr(w, k, getattr(w, k)[lo:hi])
+        w.B = hi - lo
+    else:
+        w = configs.make_c2(B=args.batch, seed=dist.shard_seed(1, rank))
     s = solver.from_workload(w, device=dev)
     # model constants: rank 0's device buffer broadcast over RCCL/xGMI (one-time, untimed)
     dist.broadcast_(s.cbuf, src=0)
     staged = s.prepare(w.X_init, w.U, w.Y)
-    B = args.batch
+    B = w.B
     outs = (torch.empty_like(staged[0]), torch.empty(B, dtype=torch.float64, device=dev),
             torch.empty(B, dtype=torch.int32, device=dev), torch.empty(B, dtype=torch.int32, device=dev))
     stream = torch.cuda.current_stream(dev)
@@ -181,12 +198,13 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": wall / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.global_batch else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (seeded van der Pol truth via RK4 + Gaussian noise, R/Q from estimation_example.py)",
             "config": {"workload": "C2 van_der_pol: n=2, m=1, full_state p=2, N=100 (P=101, d=202), T=10, M=101",
-                       "global_batch": B * world, "batch_per_gpu": B, "gn_iters_per_step": args.iters,
+                       "global_batch": args.global_batch or B * world, "batch_per_gpu": B,
+                       "gn_iters_per_step": args.iters,
                        "parallelism": f"dp{world} (independent trajectories; RCCL broadcast of constants only)"},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None,

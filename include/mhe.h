@@ -67,6 +67,8 @@ extern "C" {
 #define MHE_DYN_MULTI_RECEIVER 7         /* :81-96  n=8  m=0 */
 #define MHE_DYN_GNSS_TWO_RECEIVER 8      /* :98-115 n=10 m=6 */
 #define MHE_DYN_KINEMATIC_BICYCLE 9      /* :117-136 n=6 m=2 (kinematic_bycicle_and_bias) */
+#define MHE_DYN_GNSS_8_RECEIVERS 11      /* 8 receivers x the :98-115 block [x,y,z,b,alpha]:
+                                            n=40 m=24 */
 #define MHE_DYN_VEHICLE_GNSS 10          /* :148-174 n=9 m=2 (vehicle_dynamics_and_gnss);
                                             dyn_par = params["car_params"] as
                                             [C_AF, C_AR, M, D_F, D_R, I_Z] */
@@ -292,6 +294,20 @@ typedef struct mhe_solve_args {
 } mhe_solve_args;
 
 int mhe_solve(const mhe_dims* dims, const void* const_buf, const mhe_solve_args* args, void* stream);
+
+/*
+ * Kernel-level parity of the per-collocation-point evaluation (SURVEY §8(a) a5-a7,
+ * nlp/nlp.py:225-235 and :264-273): at X (B,P,n) with the solve's device functors,
+ *   W  (B,P,n)    W_k = (2/T) sum_j D_kj X_j - f(X_k, U_k)   (the eliminated defects)
+ *   F  (B,P,n,n)  df/dx at (X_k, U_k)
+ *   E  (B,M,p)    e_i = y_i - h(x(t_i)),  x(t_i) = sum_j Phi_ij X_j
+ *   Hm (B,M,p,n)  dh/dx at x(t_i)
+ * Any output may be NULL.  Both paths; not for MHE_MEAS_MIXED (MHE_ERR_UNSUPPORTED).
+ * A constants buffer built for other dims leaves the outputs untouched.
+ */
+int mhe_resjac(const mhe_dims* dims, const void* const_buf, int32_t batch, const double* X, const double* U,
+               int64_t u_bstride, const double* Y, const double* PAR, int64_t par_bstride, double* W,
+               double* F, double* E, double* Hm, void* stream);
 
 /*
  * Kernel-level parity: assemble the GN normal equations at X.

@@ -96,6 +96,8 @@ __host__ __device__ inline BigWs big_ws_layout(int P, int M, int n, int NT, int 
   return W;
 }
 
+constexpr int BIG_MAX_PAIRS = 44 * 45 / 2;  // component pairs (ca >= cb) of the largest model (n = 40 + z)
+
 struct BigArgs {
   const char* cbuf;
   int P, M, n, Pp, NTc, NT, q, has_prior;
@@ -124,7 +126,7 @@ struct BigArgs {
   // nonzero first ("live": both components in the measurement Jacobian's support),
   // and the k_big_assemble chunking over them (BigPairPlan)
   int npr, nlive, nchl, pchl, nch;
-  unsigned char pa[80], pb[80];
+  unsigned char pa[BIG_MAX_PAIRS], pb[BIG_MAX_PAIRS];
   double dpar[8];    // mhe_dims.dyn_par (dynamics plug-in params)
   const double* Rw;  // per-solve measurement weights (B|1, M, p, p) or NULL = the constants' Rw
   long long rwstride;
@@ -203,6 +205,67 @@ __device__ void big_active_set(const BigArgs& a, const double* X, const double* 
 }
 
 // ------------------------------------------------------------ residuals
+// Node terms for a SPARSE dynamics Jacobian (DynGnssReceivers: n = 40): E = c Qw F,
+// F^T V and F^T E accumulated from the (row, col, value) triples straight into the
+// workspace -- no n x n private array (it would live in scratch memory).
+template <class DYN>
+__device__ void big_nodes_sparse(const BigArgs& a, const BigConst& CL, const BigWs& WL, double* ws, const double* X,
+                                 int b, double& cost) {
+  constexpr int n = DYN::n, m = DYN::m, NNZ = DYN::NNZ;
+  const double* Dt = (const double*)(a.cbuf + CL.Dt);
+  const double* cw = (const double*)(a.cbuf + CL.cw);
+  const double* Qw = (const double*)(a.cbuf + CL.Qw);
+  for (int k = threadIdx.x; k < a.P; k += BIG_NTHREADS) {
+    double W[n], f[n], Fv[NNZ], uk[m > 0 ? m : 1];
+    for (int c = 0; c < n; ++c) W[c] = 0.0;
+    for (int j = 0; j < a.P; ++j) {
+      const double dv = Dt[(size_t)j * a.P + k];
+      for (int c = 0; c < n; ++c) W[c] += dv * X[j * n + c];
+    }
+    if (m > 0) {
+      const double* Up = a.U + (long long)b * a.ustride + (long long)k * m;
+      for (int c = 0; c < m; ++c) uk[c] = Up[c];
+    }
+    DYN::eval_sparse(X + k * n, uk, a.dpar, f, Fv);
+    for (int c = 0; c < n; ++c) W[c] = a.alpha * W[c] - f[c];
+    const double ck = cw[k];
+    double* Ek = ws + WL.Es + (size_t)k * n * n;
+    double* Vk = ws + WL.Vs + (size_t)k * n;
+    double* FtV = ws + WL.FtV + (size_t)k * n;
+    double* FtE = ws + WL.FtE + (size_t)k * n * n;
+    for (int c = 0; c < n * n; ++c) {
+      Ek[c] = 0.0;
+      FtE[c] = 0.0;
+    }
+    for (int r = 0; r < n; ++r) {
+      double v;
+      if (a.huber) {
+        const double q = Qw[r * n + r], dl = a.huber_delta;
+        const double sr = sqrt(1.0 + W[r] * W[r] / (dl * dl));
+        const double lam = ck * (q / sr);
+        v = lam * W[r];
+        cost += ck * (2.0 * q * dl * dl * (sr - 1.0));
+        ws[WL.LAM + k * n + r] = lam;
+        for (int z = 0; z < NNZ; ++z)
+          if (DYN::frow(z) == r) Ek[r * n + DYN::fcol(z)] = lam * Fv[z];
+      } else {
+        double s = 0.0;
+        for (int c = 0; c < n; ++c) s += Qw[r * n + c] * W[c];
+        v = ck * s;
+        cost += W[r] * v;
+        for (int z = 0; z < NNZ; ++z) Ek[r * n + DYN::fcol(z)] += ck * Qw[r * n + DYN::frow(z)] * Fv[z];
+      }
+      Vk[r] = v;
+      FtV[r] = 0.0;
+    }
+    for (int z = 0; z < NNZ; ++z) {
+      const int t = DYN::frow(z), r = DYN::fcol(z);
+      FtV[r] += Fv[z] * Vk[t];
+      for (int c = 0; c < n; ++c) FtE[r * n + c] += Fv[z] * Ek[t * n + c];
+    }
+  }
+}
+
 template <class DYN, class MEAS>
 __global__ __launch_bounds__(BIG_NTHREADS) void k_big_resid(BigArgs a, int final_pass) {
   constexpr int n = DYN::n, m = DYN::m, p = MEAS::p, q = MEAS::q;
@@ -237,6 +300,9 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_resid(BigArgs a, int final
     for (int c = 0; c < n; ++c) ws[WL.XE + e * n + c] = xe[c];
   }
   // nodes (nlp/nlp.py:225-245)
+  if constexpr (dyn_sparse<DYN>::value) {
+    big_nodes_sparse<DYN>(a, CL, WL, ws, X, b, cost);
+  } else
   for (int k = threadIdx.x; k < a.P; k += BIG_NTHREADS) {
     double dx[n], xk[n], uk[m > 0 ? m : 1], f[n], F[n * n];
     for (int c = 0; c < n; ++c) dx[c] = 0.0;
@@ -298,22 +364,29 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_resid(BigArgs a, int final
   // measurement rows grouped by epoch (nlp/nlp.py:264-273)
   if constexpr (MEAS::MIXED) {
     // scalar rows of several plug-ins over [x(t_e) ; z]; the z couplings are
-    // accumulated per epoch for k_big_border
+    // accumulated per epoch for k_big_border.  A row's gradient has at most 8 nonzeros
+    // (MHE_ROW_* codes), so its outer product is scattered straight into the epoch's
+    // blocks in the workspace (no n x n private array: n = 40 for the 8-receiver C5)
     constexpr int NA = MEAS::NA, NZX = MHE_MAX_EXTRA;
     const int nz = a.nz;
     for (int e = threadIdx.x; e < E; e += BIG_NTHREADS) {
-      double xt[NA], ge[n], G[n * n], Gz[n * NZX], Hzz[NZX * NZX], gz[NZX];
+      double* G = ws + WL.Ge + (size_t)e * n * n;
+      double* ge = ws + WL.GEe + (size_t)e * n;
+      double* Gz = ws + WL.GZe + (size_t)e * n * NZX;
+      double* Hzz = ws + WL.HZZe + (size_t)e * NZX * NZX;
+      double* gz = ws + WL.GZVe + (size_t)e * NZX;
+      double xt[NA];
       for (int c = 0; c < n; ++c) {
         xt[c] = ws[WL.XE + e * n + c];
         ge[c] = 0.0;
       }
-      for (int c = 0; c < NZX; ++c) {
-        xt[n + c] = c < nz ? a.Z[(size_t)b * nz + c] : 0.0;
-        gz[c] = 0.0;
-      }
+      for (int c = 0; c < NZX; ++c) xt[n + c] = c < nz ? a.Z[(size_t)b * nz + c] : 0.0;
       for (int c = 0; c < n * n; ++c) G[c] = 0.0;
-      for (int c = 0; c < n * NZX; ++c) Gz[c] = 0.0;
-      for (int c = 0; c < NZX * NZX; ++c) Hzz[c] = 0.0;
+      if (nz > 0) {
+        for (int c = 0; c < n * NZX; ++c) Gz[c] = 0.0;
+        for (int c = 0; c < NZX * NZX; ++c) Hzz[c] = 0.0;
+        for (int c = 0; c < NZX; ++c) gz[c] = 0.0;
+      }
       for (int i = erow[e]; i < erow[e + 1]; ++i) {
         const double* PR = a.PAR + (long long)b * a.pstride + (long long)i * q;
         const double R = Rw[i];
@@ -323,23 +396,22 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_resid(BigArgs a, int final
         const double yv = a.Y[(long long)b * a.M + i], ev = yv - h, Re = R * ev;
         cost += ev * Re;
         noise += fabs(Re) * (fabs(yv) + fabs(h));
-        for (int c = 0; c < n; ++c) {
-          ge[c] += Gr[c] * Re;
-          const double rc = R * Gr[c];
-          for (int r = 0; r < n; ++r) G[r * n + c] += Gr[r] * rc;
-          for (int z = 0; z < nz; ++z) Gz[c * NZX + z] += rc * Gr[n + z];
+        int id[8], k = 0;
+        for (int c = 0; c < NA && k < 8; ++c)
+          if (Gr[c] != 0.0) id[k++] = c;
+        for (int u = 0; u < k; ++u) {
+          const int ia = id[u];
+          const double ga = Gr[ia];
+          if (ia < n) ge[ia] += ga * Re;
+          else gz[ia - n] += ga * Re;
+          for (int v = 0; v < k; ++v) {
+            const int ib = id[v];
+            const double w2 = ga * R * Gr[ib];
+            if (ia < n && ib < n) G[ia * n + ib] += w2;
+            else if (ia < n) Gz[ia * NZX + (ib - n)] += w2;
+            else if (ib >= n) Hzz[(ia - n) * NZX + (ib - n)] += w2;
+          }
         }
-        for (int z = 0; z < nz; ++z) {
-          gz[z] += Gr[n + z] * Re;
-          for (int z2 = 0; z2 < nz; ++z2) Hzz[z * NZX + z2] += Gr[n + z] * R * Gr[n + z2];
-        }
-      }
-      for (int c = 0; c < n; ++c) ws[WL.GEe + e * n + c] = ge[c];
-      for (int c = 0; c < n * n; ++c) ws[WL.Ge + e * n * n + c] = G[c];
-      if (nz > 0) {
-        for (int c = 0; c < n * NZX; ++c) ws[WL.GZe + (size_t)e * n * NZX + c] = Gz[c];
-        for (int c = 0; c < NZX * NZX; ++c) ws[WL.HZZe + (size_t)e * NZX * NZX + c] = Hzz[c];
-        for (int c = 0; c < NZX; ++c) ws[WL.GZVe + (size_t)e * NZX + c] = gz[c];
       }
     }
   } else
@@ -456,15 +528,17 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_resid(BigArgs a, int final
 // Conservative (all components) unless the model says otherwise.
 template <class MEAS>
 struct BigGSupport {
-  static unsigned get(const int*, int n) { return (1u << n) - 1u; }
+  static unsigned long long get(const int*, int n) { return n >= 64 ? ~0ull : (1ull << n) - 1ull; }
 };
 template <int N>
 struct BigGSupport<MeasPseudorange<N>> {  // h = |x[idx0..2] - sat| + x[idx3]
-  static unsigned get(const int* idx, int) { return 1u << idx[0] | 1u << idx[1] | 1u << idx[2] | 1u << idx[3]; }
+  static unsigned long long get(const int* idx, int) {
+    return 1ull << idx[0] | 1ull << idx[1] | 1ull << idx[2] | 1ull << idx[3];
+  }
 };
 template <>
 struct BigGSupport<MeasVehiclePseudorange> {  // h = |x[0, 1, 8] - sat| + x[6]
-  static unsigned get(const int*, int) { return 1u << 0 | 1u << 1 | 1u << 8 | 1u << 6; }
+  static unsigned long long get(const int*, int) { return 1ull << 0 | 1ull << 1 | 1ull << 8 | 1ull << 6; }
 };
 
 constexpr int BIG_PCH = 5;  // pair accumulators per wave (96 VGPRs, no spills)
@@ -473,13 +547,13 @@ constexpr int BIG_PCH = 5;  // pair accumulators per wave (96 VGPRs, no spills)
 // nchl chunks of <= pchl (balanced, <= BIG_PCH) that run the epoch GEMM; the
 // pairs whose contraction is zero (e.g. the clock-drift component under
 // pseudoranges) get chunks of BIG_PCH that only write the dynamics terms.
-inline void big_pair_plan(BigArgs& A, unsigned support) {
+inline void big_pair_plan(BigArgs& A, unsigned long long support) {  // bit c: component c (n <= 44)
   const int n = A.n;
   int k = 0;
   for (int pass = 0; pass < 2; ++pass)
     for (int ca = 0; ca < n; ++ca)
       for (int cb = 0; cb <= ca; ++cb) {
-        const bool live = (support >> ca & 1u) && (support >> cb & 1u);
+        const bool live = (support >> ca & 1ull) && (support >> cb & 1ull);
         if (live == (pass == 0)) {
           A.pa[k] = (unsigned char)ca;
           A.pb[k] = (unsigned char)cb;
@@ -489,7 +563,7 @@ inline void big_pair_plan(BigArgs& A, unsigned support) {
   A.npr = k;
   int nl = 0;
   for (int ca = 0; ca < n; ++ca)
-    for (int cb = 0; cb <= ca; ++cb) nl += (support >> ca & 1u) && (support >> cb & 1u);
+    for (int cb = 0; cb <= ca; ++cb) nl += (support >> ca & 1ull) && (support >> cb & 1ull);
   A.nlive = nl;
   A.nchl = (nl + BIG_PCH - 1) / BIG_PCH;
   A.pchl = A.nchl ? (nl + A.nchl - 1) / A.nchl : 0;
@@ -1131,7 +1205,7 @@ __device__ double big_cost(const BigArgs& a, const double* X, int b, double* red
   const int Mr = a.M > 0 ? a.M : 1;
   double cost = 0.0, noise = 0.0;
   for (int k = threadIdx.x; k < a.P; k += BIG_NTHREADS) {
-    double dx[n], xk[n], uk[m > 0 ? m : 1], f[n], F[n * n];
+    double dx[n], xk[n], uk[m > 0 ? m : 1], f[n];
     for (int c = 0; c < n; ++c) dx[c] = 0.0;
     for (int j = 0; j < a.P; ++j) {
       const double dv = Dt[(size_t)j * a.P + k];
@@ -1142,7 +1216,13 @@ __device__ double big_cost(const BigArgs& a, const double* X, int b, double* red
       const double* Up = a.U + (long long)b * a.ustride + (long long)k * m;
       for (int c = 0; c < m; ++c) uk[c] = Up[c];
     }
-    DYN::eval(xk, uk, a.dpar, f, F);
+    if constexpr (dyn_sparse<DYN>::value) {
+      double Fv[DYN::NNZ];
+      DYN::eval_sparse(xk, uk, a.dpar, f, Fv);
+    } else {
+      double F[n * n];
+      DYN::eval(xk, uk, a.dpar, f, F);
+    }
     double W[n];
     for (int c = 0; c < n; ++c) W[c] = a.alpha * dx[c] - f[c];
     const double ck = cw[k];

@@ -80,7 +80,7 @@ __host__ __device__ inline ConstLayout const_layout(int P, int M, int n, int p, 
 }
 
 struct SmemLayout {  // offsets in doubles
-  int Xs, Vs, FtV, Es, FtE, GE, G, LAM, BV, YV, PB, DT, RED, ROWM, UN, XO, ACT, GV, total;
+  int Xs, Vs, FtV, Es, FtE, GE, G, LAM, BV, YV, PB, DT, RED, ROWM, UN, SIM, XO, ACT, GV, total;
 };
 
 __host__ __device__ inline int rnd2(int x) { return (x + 1) & ~1; }  // keep 16-B alignment
@@ -113,6 +113,7 @@ __host__ __device__ inline SmemLayout smem_layout(int P, int M, int n, int NT, b
   S.RED = o;  o += 4 * NW + 8;
   S.ROWM = o; o += NW * 8;              // per wave, per block row I: bit mask of its slots (I, J)
   S.UN = o;   o += UNITS;               // identity rows for the panel (unit_row)
+  S.SIM = o;  o += 8;                   // int[NW]: SIMD of each wave; int[NW]: the panel-done flag (MHE_DEFER_SIMD)
   // bounded problems only (projected Newton, k_gn<..., BOUNDED>): the iterate the
   // line search starts from, and the epsilon-active set (one int per unknown)
   S.XO = o;   o += bounded ? rnd2(P * n) : 0;
@@ -1029,6 +1030,25 @@ __device__ __forceinline__ void load_tiles(const GnArgs& a, const SmemLayout& SL
     }
 }
 
+// f64 MFMA and VALU do not co-issue on a gfx950 SIMD: while the panel
+// wave runs its ~500-instruction VALU sweep, MFMAs issued by a wave sharing its SIMD
+// stall it.  With MHE_DEFER_SIMD the waves of this workgroup on the panel wave's SIMD
+// start their trailing-update work only once the panel is done (an LDS flag).  Each
+// wave's SIMD comes from HW_REG_HW_ID (SIMD_ID, bits 5:4).
+#ifndef MHE_DEFER_SIMD
+#define MHE_DEFER_SIMD 0
+#endif
+__device__ __forceinline__ int wave_simd_id() {
+  // s_getreg_b32 HW_REG_HW_ID (id 4), offset 4, size 2
+  return __builtin_amdgcn_s_getreg((4 << 0) | (4 << 6) | ((2 - 1) << 11));
+}
+__device__ __forceinline__ void init_simd_ids(double* sim, int wave, int lane) {
+  if (lane == 0) {
+    ((int*)sim)[wave] = wave_simd_id();
+    ((int*)sim)[NW] = -2;  // panel-done flag: the step whose panel is complete
+  }
+}
+
 // LDS ordering between lanes of ONE wave: LDS operations of a wave execute in
 // order, so a compiler-level fence plus a wait on the wave's own stores suffices.
 __device__ __forceinline__ void wave_lds_sync() {
@@ -1259,7 +1279,16 @@ __device__ __forceinline__ bool factor_forward(const GnArgs& a, const SmemLayout
       }
       if (!KO(3)) bad |= panel(DTn, sm + SL.UN, lane_o);
       __builtin_amdgcn_s_setprio(0);
+      if (MHE_DEFER_SIMD && lane_o == 0)
+        __hip_atomic_store(((int*)(sm + SL.SIM)) + NW, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     } else if (k >= 0 && !KO(4)) {
+      if (MHE_DEFER_SIMD && ((const int*)(sm + SL.SIM))[wave_o] == ((const int*)(sm + SL.SIM))[pw]) {
+        // same SIMD as the panel wave: keep the MFMA pipe free until the panel is done
+        // (bounded: a wave always leaves the spin, whatever the flag says)
+        for (int spin = 0; spin < (1 << 16) &&
+             __hip_atomic_load(((int*)(sm + SL.SIM)) + NW, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != k; ++spin)
+          __builtin_amdgcn_s_sleep(1);
+      }
       // b_b -= U_kb^T y_k for b >= k + 1: one output per lane of the other waves
       const int vt = ((wave_o - pw - 1 + NW) % NW) * 64 + lane_o;
       const int bq = k + 1 + (vt >> 4), c = vt & 15;
@@ -1484,6 +1513,7 @@ __global__ __launch_bounds__(NTHREADS, NW / 2) void k_gn(GnArgs a) {  // 2nd arg
   double* Xs = sm + SL.Xs;
   if (threadIdx.x == 0) *(int*)(sm + SL.RED + 4 * NW) = 0;  // NOT_SPD flag
   init_units(sm + SL.UN);
+  init_simd_ids(sm + SL.SIM, wave, lane);
   double* DV = sm + SL.YV;  // delta after backward()
   double* RED = sm + SL.RED;
   d4 acc[SLOTS];
@@ -1684,6 +1714,7 @@ __global__ __launch_bounds__(NTHREADS, NW / 2) void k_gn_bounded(GnArgs a) {
   double* RED = sm + SL.RED;
   if (threadIdx.x == 0) *(int*)(sm + SL.RED + 4 * NW) = 0;  // NOT_SPD flag
   init_units(sm + SL.UN);
+  init_simd_ids(sm + SL.SIM, wave, lane);
   d4 acc[SLOTS];
 #pragma unroll
   for (int s = 0; s < SLOTS; ++s) acc[s] = d4{0.0, 0.0, 0.0, 0.0};
@@ -1877,6 +1908,7 @@ inline bool dyn_info(int id, int& n, int& m) {
     case MHE_DYN_GNSS_TWO_RECEIVER: n = 10; m = 6; return true;
     case MHE_DYN_KINEMATIC_BICYCLE: n = 6; m = 2; return true;
     case MHE_DYN_VEHICLE_GNSS: n = 9; m = 2; return true;
+    case MHE_DYN_GNSS_8_RECEIVERS: n = 40; m = 24; return true;
   }
   return false;
 }
@@ -1921,6 +1953,96 @@ inline size_t big_ws_doubles(const mhe_dims* dm, int NT) {
   return big_ws_layout(dm->N + 1, dm->M, dm->n, NT, dm->n_extra, dm->n_eq).total;
 }
 
+// ------------------------------------------------------------ resjac (kernel-level parity)
+// Per-collocation-point residuals and Jacobians at X, one thread per
+// (trajectory, node) and per (trajectory, row): W_k = a sum_j D_kj X_j - f(X_k, U_k),
+// F_k = df/dx; e_i = y_i - h(x(t_i)), Hm_i = dh/dx at x(t_i) = sum_j Phi_ij X_j.  The
+// same device functors and constants as the solve; Phi from the register layout or, on
+// the large-system path, from the epoch-compressed rows (row i -> its epoch by erow).
+struct ResjacArgs {
+  const char* cbuf;
+  int P, M, big;
+  double alpha;
+  const double *X, *U, *Y, *PAR;
+  long long ustride, pstride;
+  double *W, *F, *E, *Hm;
+  int idx[8];
+  double dpar[8];
+  unsigned long long tag;
+};
+
+template <class DYN, class MEAS>
+__global__ void k_resjac(ResjacArgs a, int batch) {
+  constexpr int n = DYN::n, m = DYN::m, p = MEAS::p, q = MEAS::q;
+  const int P = a.P, M = a.M;
+  const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (long long)batch * (P + M)) return;
+  if (*(const unsigned long long*)a.cbuf != a.tag) return;  // constants built for other dims
+  const int b = (int)(gid / (P + M)), t = (int)(gid % (P + M));
+  const double* X = a.X + (size_t)b * P * n;
+  const double *D, *Phi = nullptr, *PhiE = nullptr;
+  const int* erow = nullptr;
+  int E = 0;
+  if (a.big) {
+    const BigConst CL = big_const_layout(P, M, n, p);
+    D = (const double*)(a.cbuf + CL.D);
+    PhiE = (const double*)(a.cbuf + CL.PhiE);
+    erow = (const int*)(a.cbuf + CL.erow);
+    E = M > 0 ? *(const int*)(a.cbuf + CL.ne) : 0;
+  } else {
+    const ConstLayout CL = const_layout(P, M, n, p, 1);
+    D = (const double*)(a.cbuf + CL.D);
+    Phi = (const double*)(a.cbuf + CL.Phi);
+  }
+  if (t < P) {
+    const int k = t;
+    double dx[n], xk[n], uk[m > 0 ? m : 1], f[n], F[n * n];
+    for (int c = 0; c < n; ++c) dx[c] = 0.0;
+    for (int j = 0; j < P; ++j)
+      for (int c = 0; c < n; ++c) dx[c] += D[(size_t)k * P + j] * X[j * n + c];
+    for (int c = 0; c < n; ++c) xk[c] = X[k * n + c];
+    if (m > 0)
+      for (int c = 0; c < m; ++c) uk[c] = a.U[(long long)b * a.ustride + (long long)k * m + c];
+    DYN::eval(xk, uk, a.dpar, f, F);
+    if (a.W)
+      for (int c = 0; c < n; ++c) a.W[((size_t)b * P + k) * n + c] = a.alpha * dx[c] - f[c];
+    if (a.F)
+      for (int c = 0; c < n * n; ++c) a.F[((size_t)b * P + k) * n * n + c] = F[c];
+    return;
+  }
+  const int i = t - P;
+  const double* phi = Phi ? Phi + (size_t)i * P : nullptr;
+  if (!phi) {  // large-system path: the row's epoch
+    int lo = 0, hi = E - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) / 2;
+      if (erow[mid] <= i) lo = mid; else hi = mid - 1;
+    }
+    phi = PhiE + (size_t)lo * P;
+  }
+  double xi[n], par[q > 0 ? q : 1], h[p], H[p * n];
+  for (int c = 0; c < n; ++c) xi[c] = 0.0;
+  for (int j = 0; j < P; ++j)
+    for (int c = 0; c < n; ++c) xi[c] += phi[j] * X[j * n + c];
+  for (int c = 0; c < q; ++c) par[c] = a.PAR[(long long)b * a.pstride + (long long)i * q + c];
+  MEAS::eval(xi, par, a.idx, h, H);
+  if (a.E)
+    for (int r = 0; r < p; ++r) a.E[((size_t)b * M + i) * p + r] = a.Y[((size_t)b * M + i) * p + r] - h[r];
+  if (a.Hm)
+    for (int c = 0; c < p * n; ++c) a.Hm[((size_t)b * M + i) * p * n + c] = H[c];
+}
+
+template <class DYN, class MEAS>
+int launch_resjac(ResjacArgs& a, int batch, hipStream_t st) {
+  if constexpr (MEAS::MIXED) {
+    return MHE_ERR_UNSUPPORTED;  // mixed rows: see mhe_solve parity tests
+  } else {
+    const long long nt = (long long)batch * (a.P + a.M);
+    hipLaunchKernelGGL((k_resjac<DYN, MEAS>), dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, st, a, batch);
+    return hipGetLastError() == hipSuccess ? MHE_OK : MHE_ERR_HIP;
+  }
+}
+
 // Per (dynamics, measurement) pair: the launches that depend on the model types.
 struct PairOps {
   // register-resident path: the tile tables of the constants buffer (k_build_cc)
@@ -1932,6 +2054,8 @@ struct PairOps {
   // -> update / line search, then the final residual pass (A.X holds X0 and the
   // state words are initialised by the caller)
   int (*big)(const mhe_dims* dm, BigArgs& A, int batch, int max_iter, hipStream_t st);
+  // kernel-level parity: residuals and Jacobians per node / row (mhe_resjac)
+  int (*resjac)(ResjacArgs& a, int batch, hipStream_t st);
 };
 
 template <class DYN, class MEAS>
@@ -2014,7 +2138,8 @@ int launch_big(const mhe_dims* dm, BigArgs& A, int batch, int max_iter, hipStrea
 
 template <class DYN, class MEAS>
 const PairOps* pair_ops() {
-  static const PairOps ops = {&launch_build_cc<DYN, MEAS>, &launch_gn<DYN, MEAS>, &launch_big<DYN, MEAS>};
+  static const PairOps ops = {&launch_build_cc<DYN, MEAS>, &launch_gn<DYN, MEAS>, &launch_big<DYN, MEAS>,
+                              &launch_resjac<DYN, MEAS>};
   return &ops;
 }
 
@@ -2023,5 +2148,6 @@ const PairOps* pairs_vdp(int dyn, int meas);
 const PairOps* pairs_integrators(int dyn, int meas);
 const PairOps* pairs_gnss(int dyn, int meas);
 const PairOps* pairs_vehicles(int dyn, int meas);
+const PairOps* pairs_receivers(int dyn, int meas);
 
 }  // namespace mhe

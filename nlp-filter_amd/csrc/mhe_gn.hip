@@ -170,6 +170,7 @@ const PairOps* find_pair(const mhe_dims* dm) {
   if (!ops) ops = pairs_integrators(dm->dyn_model, dm->meas_model);
   if (!ops) ops = pairs_gnss(dm->dyn_model, dm->meas_model);
   if (!ops) ops = pairs_vehicles(dm->dyn_model, dm->meas_model);
+  if (!ops) ops = pairs_receivers(dm->dyn_model, dm->meas_model);
 #endif
   return ops;
 }
@@ -426,6 +427,31 @@ int mhe_solve(const mhe_dims* dims, const void* const_buf, const mhe_solve_args*
   a.pstride = g->par_bstride; a.x0 = g->x0; a.cost = g->cost_out; a.iters = g->iters_out; a.status = g->status_out;
   a.max_iter = g->max_iter; a.tol = g->tol; a.Rw = g->Rw; a.rwstride = g->rw_bstride;
   return ops->gn(dims, a, batch, MODE_SOLVE, st);
+}
+
+int mhe_resjac(const mhe_dims* dims, const void* const_buf, int32_t batch, const double* X, const double* U,
+               int64_t u_bstride, const double* Y, const double* PAR, int64_t par_bstride, double* W, double* F,
+               double* E, double* Hm, void* stream) {
+  int NT = 0;
+  int rc = check_dims(dims, &NT);
+  if (rc != MHE_OK) return rc;
+  if (dims->meas_model == MHE_MEAS_MIXED) return MHE_ERR_UNSUPPORTED;
+  if (batch <= 0) return batch == 0 ? MHE_OK : MHE_ERR_DIMS;
+  if (!const_buf || !X || (dims->m > 0 && !U) || (dims->M > 0 && E && !Y) || (dims->q > 0 && dims->M > 0 && !PAR))
+    return MHE_ERR_NULL;
+  const PairOps* ops = find_pair(dims);
+  if (!ops) return MHE_ERR_UNSUPPORTED;
+  ResjacArgs a = {};
+  a.cbuf = (const char*)const_buf;
+  a.P = dims->N + 1; a.M = dims->M; a.big = is_big(dims) ? 1 : 0; a.alpha = 2.0 / dims->T;
+  a.X = X; a.U = U; a.ustride = u_bstride; a.Y = Y; a.PAR = PAR; a.pstride = par_bstride;
+  a.W = W; a.F = F; a.E = E; a.Hm = Hm;
+  for (int i = 0; i < 8; ++i) {
+    a.idx[i] = dims->meas_idx[i];
+    a.dpar[i] = dims->dyn_par[i];
+  }
+  a.tag = const_tag(dims, NT);
+  return ops->resjac(a, batch, (hipStream_t)stream);
 }
 
 int mhe_assemble(const mhe_dims* dims, const void* const_buf, int32_t batch, const double* X, const double* U,

@@ -122,6 +122,47 @@ struct DynKinematicBicycle {
   }
 };
 
+// R receivers, each the per-receiver block of gnss_two_receiver (nlp/dynamics.py:98-115):
+// x = [x, y, z, b, alpha] per receiver (n = 5R), u = receiver velocities (m = 3R);
+// xdot_r = u_r, bdot_r = alpha_r, alphadot_r = 0.  SURVEY.md §8(d) C5 (R = 8, n = 40).
+// The Jacobian has R nonzeros (d b_r / d alpha_r = 1): SPARSE functors also give it as
+// (row, col, value) triples so the large-system path never forms an n x n array.
+template <int R_>
+struct DynGnssReceivers {
+  static constexpr int n = 5 * R_, m = 3 * R_;
+  static constexpr bool SPARSE = true;
+  static constexpr int NNZ = R_;
+  __device__ static int frow(int k) { return 5 * k + 3; }
+  __device__ static int fcol(int k) { return 5 * k + 4; }
+  __device__ static void eval_sparse(const double* x, const double* u, const double*, double* f, double* Fv) {
+#pragma unroll
+    for (int r = 0; r < R_; ++r) {
+      f[5 * r + 0] = u[3 * r + 0];
+      f[5 * r + 1] = u[3 * r + 1];
+      f[5 * r + 2] = u[3 * r + 2];
+      f[5 * r + 3] = x[5 * r + 4];
+      f[5 * r + 4] = 0.0;
+      Fv[r] = 1.0;
+    }
+  }
+  __device__ static void eval(const double* x, const double* u, const double* dp, double* f, double* F) {
+    double Fv[NNZ];
+    eval_sparse(x, u, dp, f, Fv);
+    for (int i = 0; i < n * n; ++i) F[i] = 0.0;
+    for (int k = 0; k < NNZ; ++k) F[frow(k) * n + fcol(k)] = Fv[k];
+  }
+};
+
+// SPARSE detection: functors without the member are dense
+template <class DYN, class = void>
+struct dyn_sparse {
+  static constexpr bool value = false;
+};
+template <class DYN>
+struct dyn_sparse<DYN, decltype(void(DYN::SPARSE))> {
+  static constexpr bool value = DYN::SPARSE;
+};
+
 // nlp/dynamics.py:148-174  vehicle_dynamics_and_gnss: x = [px, py, psi, vx, vy, r, b, bd, pz],
 // u = [F_xr, delta]; the dynamic bicycle of vehicle_dynamics (:148-164, linear tyres with
 // vx + 0.001 in the slip angles) plus bdot = bd.  dp = params["car_params"] as

@@ -74,6 +74,8 @@ SIGNATURES = {
     "mhe_gn_solve_ext": (ctypes.c_int, [_P, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64,
                                         c_vp, c_vp, c_vp, c_vp, c_i32, c_dbl, c_vp, c_sz, c_vp]),
     "mhe_solve": (ctypes.c_int, [_P, c_vp, ctypes.POINTER(MheSolveArgs), c_vp]),
+    "mhe_resjac": (ctypes.c_int, [_P, c_vp, c_i32, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp,
+                                  c_vp]),
     "mhe_assemble": (ctypes.c_int, [_P, c_vp, c_i32, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp,
                                     c_vp, c_vp, c_vp, c_vp]),
     "mhe_chol_solve": (ctypes.c_int, [_P, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),

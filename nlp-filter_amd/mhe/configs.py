@@ -109,20 +109,28 @@ def make_c2(B=1024, seed=1, N=100):
 
 
 
-def make_gnss_small(B=4, seed=2, N=10, T=50.0, n_sat=8, epochs=51):
+def make_gnss_small(B=4, seed=2, N=10, T=50.0, n_sat=8, epochs=51, sat=None, count=None):
     """Small gnss_stationary-shaped problem (pseudorange, n=5) for parity tests.
 
-    Synthetic ENU satellite positions at ~2e7 m (fixed per slot over the
-    window, shared by the batch); truth = stationary receiver + drifting clock.
-    Q, r_pr as gnss_stationary.py:18-19.
+    Satellite ENU positions: ``sat`` (epochs, n_sat, 3) when given (time-varying; slots
+    j >= count[e] are empty: R = 0 and a zero position, as the reference masks them,
+    autonomous-car.py:260-263), else synthetic ones at ~2e7 m fixed per slot, shared by
+    the batch.  Truth = stationary receiver + drifting clock; Q, r_pr as
+    gnss_stationary.py:18-19.
     """
     rng = np.random.default_rng(seed)
     t_ep = np.linspace(0, T, epochs)
-    az = rng.uniform(0, 2 * np.pi, n_sat)
-    el = rng.uniform(0.3, 1.3, n_sat)
-    sat = 2.2e7 * np.stack([np.cos(el) * np.cos(az), np.cos(el) * np.sin(az), np.sin(el)], axis=1)
+    if sat is None:
+        az = rng.uniform(0, 2 * np.pi, n_sat)
+        el = rng.uniform(0.3, 1.3, n_sat)
+        s0 = 2.2e7 * np.stack([np.cos(el) * np.cos(az), np.cos(el) * np.sin(az), np.sin(el)], axis=1)
+        sat = np.broadcast_to(s0, (epochs, n_sat, 3)).copy()
+    sat = np.asarray(sat, dtype=np.float64)[:epochs]
+    n_sat = sat.shape[1]
+    live = np.ones((epochs, n_sat), dtype=bool) if count is None else (np.arange(n_sat)[None, :] < np.asarray(count)[:epochs, None])
+    sat = np.where(live[..., None], sat, 0.0)
     t_meas = np.repeat(t_ep, n_sat)
-    PAR = np.tile(sat, (epochs, 1))[None]  # (1, M, 3)
+    PAR = sat.reshape(1, -1, 3)  # (1, M, 3)
     M = t_meas.shape[0]
     pos = rng.normal(size=(B, 3)) * 10.0
     b0 = rng.normal(size=B) * 100.0
@@ -132,8 +140,8 @@ def make_gnss_small(B=4, seed=2, N=10, T=50.0, n_sat=8, epochs=51):
     xt[:, :, :3] = pos[:, None, :]
     xt[:, :, 3] = b0[:, None] + bd[:, None] * t_ep[None, :]
     xt[:, :, 4] = bd[:, None]
-    rho = np.linalg.norm(xt[:, :, None, :3] - sat[None, None, :, :], axis=-1) + xt[:, :, None, 3]
-    Y = (rho + rng.normal(size=rho.shape) * np.sqrt(r_pr)).reshape(B, M, 1)
+    rho = np.linalg.norm(xt[:, :, None, :3] - sat[None, :, :, :], axis=-1) + xt[:, :, None, 3]
+    Y = np.where(live[None], rho + rng.normal(size=rho.shape) * np.sqrt(r_pr), 0.0).reshape(B, M, 1)
     cpm = ChebyshevPseudospectralMethod(N, 0, T)
     t_nodes = cpm.tau2t(cpm.tau)
     X_init = np.zeros((B, N + 1, 5))
@@ -141,17 +149,29 @@ def make_gnss_small(B=4, seed=2, N=10, T=50.0, n_sat=8, epochs=51):
     X_init[:, :, 3] = (b0[:, None] + bd[:, None] * t_nodes[None, :]) + rng.normal(size=(B, 1)) * 3.0
     X_init[:, :, 4] = bd[:, None]
     Q = np.diag([0.0001, 0.0001, 0.0001, 0.1, 0.001])
+    Rw = np.where(live.reshape(-1), 1.0 / r_pr, 0.0)[:, None, None]
     return Workload(name="gnss_small", N=N, T=T, n=5, m=3, p=1, M=M, B=B,
                     dyn="gnss_pos_and_bias", meas="pseudorange", meas_static={"idx": [0, 1, 2, 3]},
                     t_meas=t_meas, Y=Y, U=np.zeros((1, N + 1, 3)), PAR=PAR, Qw=np.linalg.inv(Q),
-                    Rw=np.full((M, 1, 1), 1.0 / r_pr), Pw=None, x0=None, X_init=X_init, X_true=xt, cpm=cpm)
+                    Rw=Rw, Pw=None, x0=None, X_init=X_init, X_true=xt, cpm=cpm)
+
+
+def c3_geometry():
+    """The satellite geometry of the reference's gnss_stationary log (201 epochs x 12
+    slots, ENU; tests/golden/gnss_stationary_c3.npz, generated by the reference's own
+    load_gnss_logs / ecef2enu in tests/golden/gen_golden.py)."""
+    import os
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "tests", "golden", "gnss_stationary_c3.npz")
+    z = np.load(path)
+    return z["sat_enu"], z["count"]
 
 
 def make_c3(B=4096, seed=2, N=200):
     """C3 gnss_stationary shape: gnss_pos_and_bias (n=5, m=3, u=0) +
-    pseudorange, N=200, T=200 s, 201 epochs x 12 satellite slots (M=2412), d=1005.
-    Synthetic satellite geometry (the reference's .mat ephemerides stay off the box)."""
-    w = make_gnss_small(B=B, seed=seed, N=N, T=200.0, n_sat=12, epochs=201)
+    pseudorange, N=200, T=200 s, 201 epochs x 12 satellite slots (M=2412), d=1005, with
+    the satellite positions of data/gnss_stationary's log (empty slots: R = 0)."""
+    sat, cnt = c3_geometry()
+    w = make_gnss_small(B=B, seed=seed, N=N, T=200.0, epochs=201, sat=sat, count=cnt)
     w.name = "C3_gnss_stationary"
     return w
 
@@ -214,8 +234,19 @@ def make_c4(B=1024, seed=3, N=500, epochs=None, n_sat=12):
                     X_init=X_init, X_true=xt, cpm=cpm)
 
 
-def make_c5(B=2048, seed=4, N=200, epochs=None, n_sat=12):
-    """C5 multi-receiver shape: multi_receiver dynamics (x = [p, b, v, alpha], n=8, m=0),
+def pr_row(idx, sat):
+    """MHE_MEAS_MIXED PSEUDORANGE row (include/mhe.h): [1, i0..i3, -1 x 3, sat, 0 x 3]."""
+    return [1.0] + [float(i) for i in idx] + [-1.0] * 3 + list(np.asarray(sat, dtype=np.float64)) + [0.0] * 3
+
+
+def range3d_row(idx):
+    """MHE_MEAS_MIXED RANGE_3D row between x[idx[0:3]] and x[idx[3:6]], offset 0."""
+    return [4.0] + [float(i) for i in idx] + [-1.0] + [0.0] * 6
+
+
+def make_c5_small(B=2048, seed=4, N=200, epochs=None, n_sat=12):
+    """C5s (an extra config, NOT SURVEY §8(d)'s C5): the reference's own multi-receiver.py
+    structure -- multi_receiver dynamics (x = [p, b, v, alpha], n=8, m=0),
     per epoch 12 pseudoranges + 12 pseudorange rates (sat_pos, sat_vel) and one 2-D range
     to XA (extra decision variable, 3 components; multi-receiver.py:73,99), mixed rows
     (include/mhe.h).  Weights as multi-receiver.py:77-88 (the script passes inv(Q))."""
@@ -264,7 +295,7 @@ def make_c5(B=2048, seed=4, N=200, epochs=None, n_sat=12):
     xt[:, :, 7] = al[:, None]
     X_init = xt + rng.normal(size=(B, 1, 8)) * np.array([2.0, 2.0, 2.0, 2.0, 0.05, 0.05, 0.05, 0.05])
     Q = np.diag([0.01, 0.01, 0.01, 0.01, 1., 1., 0.01, 0.01])
-    return Workload(name="C5_multi_receiver", N=N, T=T, n=8, m=0, p=1, M=M, B=B,
+    return Workload(name="C5s_multi_receiver_n8", N=N, T=T, n=8, m=0, p=1, M=M, B=B,
                     dyn="multi_receiver", meas="mixed", meas_static={}, n_extra=3,
                     t_meas=np.asarray(t_rows), Y=np.stack(Yl, axis=1)[:, :, None], U=None,
                     PAR=np.asarray(rows, dtype=np.float64)[None], Qw=np.linalg.inv(Q), Rw=np.asarray(Rw),
@@ -272,4 +303,64 @@ def make_c5(B=2048, seed=4, N=200, epochs=None, n_sat=12):
                     X_true=xt, Z_true=xa, cpm=cpm)
 
 
-CONFIGS.update({"C4": make_c4, "C5": make_c5})
+def make_c5(B=2048, seed=4, N=200, R=8, r_pr=1.0, r_range=0.01, spacing=5.0):
+    """C5 as SURVEY.md §8(d) defines it: 8 receivers, each the per-receiver block of
+    gnss_two_receiver [x, y, z, b, alpha] (nlp/dynamics.py:98-115) -> n = 40, m = 24
+    (each receiver's velocity as its control, as gnss-multi-receiver.py:156-165 feeds
+    LS velocities); per epoch 12 pseudoranges per receiver (idx offsets 5r, the
+    satellite epochs of data/gnss_stationary's log, empty slots R = 0) and one
+    multi_receiver_range_3d row between each adjacent pair (nlp/measurements.py:39-54),
+    mixed rows (include/mhe.h).  N = 200, T = 200 s, 201 epochs x (96 + 7) rows, d = 8040.
+    Weights as gnss-multi-receiver.py:43-48 (Q per receiver block, r_pr = 1 (B's),
+    r_range = 0.01, dt = 1 s).  Receivers in a line `spacing` m apart, moving together."""
+    T = float(N)
+    epochs = N + 1
+    rng = np.random.default_rng(seed)
+    sat_all, cnt = c3_geometry()
+    sat_all, cnt = sat_all[:epochs], cnt[:epochs]
+    t_ep = np.linspace(0, T, epochs)
+    n, m = 5 * R, 3 * R
+    p0 = rng.normal(size=(B, 3)) * 10.0
+    hd = rng.uniform(0, 2 * np.pi, B)
+    vel = np.stack([np.cos(hd), np.sin(hd), np.zeros(B)], axis=1) * rng.uniform(0.5, 1.5, (B, 1))
+    side = np.stack([-np.sin(hd), np.cos(hd), np.zeros(B)], axis=1)
+    b0 = rng.normal(size=(B, R)) * 100.0
+    al = rng.normal(size=(B, R)) * 0.5
+    offs = (np.arange(R) - (R - 1) / 2.0) * spacing                     # positions along the line
+    rows, t_rows, Rw, Yl = [], [], [], []
+    for k, tk in enumerate(t_ep):
+        base = p0 + vel * tk                                             # (B, 3)
+        pos = base[:, None, :] + offs[None, :, None] * side[:, None, :]  # (B, R, 3)
+        for r in range(R):
+            for j in range(sat_all.shape[1]):
+                live = j < cnt[k]
+                sp = sat_all[k, j] if live else np.zeros(3)
+                rows.append(pr_row([5 * r, 5 * r + 1, 5 * r + 2, 5 * r + 3], sp))
+                t_rows.append(tk); Rw.append(1.0 / r_pr if live else 0.0)
+                rho = np.linalg.norm(pos[:, r] - sp, axis=1) + b0[:, r] + al[:, r] * tk
+                Yl.append(np.where(live, rho + rng.normal(size=B) * np.sqrt(r_pr), 0.0))
+        for r in range(R - 1):
+            rows.append(range3d_row([5 * r, 5 * r + 1, 5 * r + 2, 5 * r + 5, 5 * r + 6, 5 * r + 7]))
+            t_rows.append(tk); Rw.append(1.0 / r_range)
+            d = np.sqrt(np.sum((pos[:, r] - pos[:, r + 1]) ** 2, axis=1) + 1e-6)
+            Yl.append(d + rng.normal(size=B) * np.sqrt(r_range))
+    M = len(rows)
+    cpm = ChebyshevPseudospectralMethod(N, 0, T)
+    t_nodes = cpm.tau2t(cpm.tau)
+    xt = np.zeros((B, t_nodes.shape[0], n))
+    for r in range(R):
+        pr_ = (p0[:, None] + vel[:, None] * t_nodes[None, :, None]) + offs[r] * side[:, None]
+        xt[:, :, 5 * r:5 * r + 3] = pr_
+        xt[:, :, 5 * r + 3] = b0[:, r:r + 1] + al[:, r:r + 1] * t_nodes[None]
+        xt[:, :, 5 * r + 4] = al[:, r:r + 1]
+    U = np.repeat(np.tile(vel, (1, R))[:, None, :], t_nodes.shape[0], axis=1) + rng.normal(size=(B, 1, m)) * 0.05
+    X_init = xt + rng.normal(size=(B, 1, n)) * np.tile([2.0, 2.0, 2.0, 2.0, 0.05], R)
+    Qd = np.tile([.01, .01, .01, 0.01, 0.01], R)                         # gnss-multi-receiver.py:43
+    return Workload(name="C5_eight_receivers", N=N, T=T, n=n, m=m, p=1, M=M, B=B,
+                    dyn="gnss_eight_receivers", meas="mixed", meas_static={}, n_extra=0,
+                    t_meas=np.asarray(t_rows), Y=np.stack(Yl, axis=1)[:, :, None], U=U,
+                    PAR=np.asarray(rows, dtype=np.float64)[None], Qw=np.diag(1.0 / Qd), Rw=np.asarray(Rw),
+                    Pw=None, x0=None, X_init=X_init, X_true=xt, cpm=cpm)
+
+
+CONFIGS.update({"C4": make_c4, "C5": make_c5, "C5s": make_c5_small})

@@ -29,6 +29,7 @@ DYN = {
     "gnss_two_receiver": (8, 10, 6),        # :98-115
     "kinematic_bycicle_and_bias": (9, 6, 2),  # :117-136
     "vehicle_dynamics_and_gnss": (10, 9, 2),  # :148-174 (params["car_params"] -> dyn_par)
+    "gnss_eight_receivers": (11, 40, 24),     # 8 x the :98-115 receiver block (C5, n = 40)
 }
 
 # Static parameters of the device functors (mhe_dims.dyn_par), from the plug-in's params
@@ -82,6 +83,7 @@ COMPILED_PAIRS = {
     ("gnss_pos_and_bias", "mixed"),
     ("kinematic_bycicle_and_bias", "mixed"),
     ("vehicle_dynamics_and_gnss", "mixed"),
+    ("gnss_eight_receivers", "mixed"),
 }
 
 

@@ -313,6 +313,23 @@ class BatchSolver:
         with launch_stream(stream, self.device, (self._built,)) as (s, cur):
             self._gn(s, cur, B, X, Xo, U_t, ustr, Y_t, PAR_t, pstr, x0_t, cost, iters, status, max_iter, tol)
 
+    def resjac(self, X, U, Y, PAR=None, stream=None):
+        """Per-node defects W (B,P,n) and dynamics Jacobians F (B,P,n,n), per-row
+        residuals E (B,M,p) and measurement Jacobians Hm (B,M,p,n) at X (mhe_resjac)."""
+        with launch_stream(stream, self.device, (self._built,)) as (s, cur):
+            X, B, U_t, ustr, Y_t, PAR_t, pstr, _ = self._inputs(X, U, Y, PAR, np.zeros((X.shape[0], self.n))
+                                                                if self.dims.has_prior else None)
+            f64 = dict(dtype=torch.float64, device=self.device)
+            W = torch.empty((B, self.P, self.n), **f64)
+            F = torch.empty((B, self.P, self.n, self.n), **f64)
+            E = torch.empty((B, self.M, self.p), **f64)
+            Hm = torch.empty((B, self.M, self.p, self.n), **f64)
+            rc = self.lib.mhe_resjac(self.dims, _ptr(self.cbuf), B, _ptr(X), _ptr(U_t), ustr, _ptr(Y_t), _ptr(PAR_t),
+                                     pstr, _ptr(W), _ptr(F), _ptr(E), _ptr(Hm), _handle(s))
+            _lib.check(rc, "mhe_resjac")
+            keep_alive(s, cur, X, U_t, Y_t, PAR_t, W, F, E, Hm)
+        return W, F, E, Hm
+
     def assemble(self, X, U, Y, PAR=None, x0=None, stream=None):
         """GN normal equations at X: H (B,dp,dp), g (B,dp), cost (B)."""
         with launch_stream(stream, self.device, (self._built,)) as (s, cur):

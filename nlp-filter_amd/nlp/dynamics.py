@@ -76,3 +76,10 @@ def vehicle_dynamics_and_gnss(x, u, params=None):
     """x = [px, py, psi, vx, vy, psid, b, bd, pz]: vehicle_dynamics plus bdot = bd
     (nlp/dynamics.py:166-174; autonomous-car.py:192)."""
     return vertcat(vehicle_dynamics(x[:6], u, params), x[7], 0.0, 0.0)
+
+
+def gnss_eight_receivers(x, u, params=None):
+    """Eight receivers, each the per-receiver block of gnss_two_receiver
+    (nlp/dynamics.py:98-115): x = [x, y, z, b, alpha] x 8 (n = 40), u = the receivers'
+    velocities (m = 24).  The SURVEY.md §8(d) C5 joint state ("~4N dims, N = 8")."""
+    return vertcat(*[vertcat(u[3 * r], u[3 * r + 1], u[3 * r + 2], x[5 * r + 4], 0.0) for r in range(8)])

@@ -14,9 +14,15 @@ Rules (enforced by review, see DESIGN.md "Oracle"):
 Pinning: the constants (tau, D, w, poly1d phi) and the plug-in values/Jacobians
 are pinned against golden vectors produced by the reference itself
 (``tests/golden/gen_golden.py``, run in the build container where
-``/root/reference`` exists); the EKF against the reference's stored
-``data/autonomous-car/filtering/ekf.pkl`` trajectory. The Gauss-Newton optimum
-of the IPOPT path is NOT pinnable here (CasADi/IPOPT absent): it is checked
-against ``scipy.optimize.least_squares`` on the same objective instead
-("parity unpinned" for IPOPT itself).
+``/root/reference`` exists); the EKF against the reference EKF run on the
+gnss_stationary log (``tests/golden/ekf_gnss_stationary.npz``, 51 steps, bit-exact);
+the least-squares initialiser against reference runs on seeded logs and against the
+stored ``data/gnss-multi-receiver/LS_{A,B}.csv`` (tests/test_multi_receiver.py).  The
+stored result pickles (``ekf.pkl``, ``nlp-{l2,huber}.pkl``, ``nlp.pkl``) are NOT used:
+the only loader permitted for files shipped in the reference, torch.load(weights_only=
+True), refuses these Python-2 pickles.  The Gauss-Newton optimum of the
+IPOPT path is NOT pinnable here (CasADi/IPOPT absent): it is checked against
+``scipy.optimize.least_squares`` on the same objective instead ("parity unpinned" for
+IPOPT itself); the one stored IPOPT output that can be read
+(``NLP_{A,B}.csv``) is shown not to be the optimum of the script's objective.
 """

@@ -13,6 +13,7 @@ Dynamics  f(x, u) -> (f (..., n), F = df/dx (..., n, n))
   gnss_two_receiver            nlp/dynamics.py:98-115
   kinematic_bycicle_and_bias   nlp/dynamics.py:117-136 (uses x[2] as the heading,
                                exactly as the reference code does)
+  gnss_eight_receivers         8 x the receiver block of nlp/dynamics.py:98-115 (C5, n=40)
   vehicle_dynamics_and_gnss    nlp/dynamics.py:148-174 (static = params["car_params"]:
                                a dict with C_AF, C_AR, M, D_F, D_R, I_Z as
                                utils/vehicle_sim.py:10-23, or that 6-vector)
@@ -77,6 +78,14 @@ def dyn_eval(name, x, u, static=None):
         F[..., 0, 2] = -v * np.sin(x[..., 2])
         F[..., 1, 2] = v * np.cos(x[..., 2])
         F[..., 3, 4] = 1.0
+    elif name == "gnss_eight_receivers":
+        # 8 x the per-receiver block of gnss_two_receiver (nlp/dynamics.py:98-115)
+        z = np.zeros_like(x[..., 0])
+        cols = []
+        for r in range(8):
+            cols += [u[..., 3 * r], u[..., 3 * r + 1], u[..., 3 * r + 2], x[..., 5 * r + 4], z]
+            F[..., 5 * r + 3, 5 * r + 4] = 1.0
+        f = np.stack(cols, axis=-1)
     elif name == "vehicle_dynamics_and_gnss":
         C = static
         if isinstance(C, dict):

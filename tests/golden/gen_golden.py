@@ -420,10 +420,29 @@ def gen_least_squares(ref):
     np.savez_compressed(os.path.join(OUT, "least_squares.npz"), **out)
 
 
+def gen_c3_geometry(ref):
+    """the satellite geometry of data/gnss_stationary's log -- the
+    first 201 epochs of 12 slots, loaded by the reference's own load_gnss_logs and
+    rotated to ENU at the scripts' reference point by its ecef2enu
+    (gnss_stationary.py:19-31 recipe).  Slots an epoch lacks are flagged (count)."""
+    data = ref.data.load_gnss_logs(f"{REF}/data/gnss_stationary/gnss_log_2020_02_05_09_14_15")
+    p_ref = ref.gutils.lla2ecef(np.array([37.4276, -122.1670, 0.0]))
+    E, S = 201, 12
+    sat = np.zeros((E, S, 3))
+    cnt = np.zeros(E, dtype=np.int32)
+    for k in range(E):
+        sp = data["sat_pos"][k]
+        cnt[k] = sp.shape[0]
+        for j in range(cnt[k]):
+            sat[k, j] = ref.gutils.ecef2enu(sp[j, :], p_ref)
+    np.savez_compressed(os.path.join(OUT, "gnss_stationary_c3.npz"), sat_enu=sat, count=cnt,
+                        t=np.asarray(list(data["t"]), dtype=np.float64)[:E])
+
+
 def main(which=None):
     ref = load_reference()
     gens = {"collocation": gen_collocation, "plugins": gen_plugins, "ekf": gen_ekf, "gnss_io": gen_gnss_io,
-            "least_squares": gen_least_squares}
+            "least_squares": gen_least_squares, "c3_geometry": gen_c3_geometry}
     for name, fn in gens.items():
         if not which or name in which:
             fn(ref)

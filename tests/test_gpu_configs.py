@@ -6,9 +6,13 @@ large-system path, against the oracle.
   8 floor + 1e-10 (1 + max|X|) (tests/tolerance.py: floor = the oracle's own change
   when every y, or every entry of H and g, moves by eps of its magnitude) -- ~1 cm
   here: moving H by eps moves X by ~1 mm at N = 500 (cond(H)), whatever the order.
-* C5 (mixed rows: pseudorange, pseudorange rate, 2-D range to the extra variable
-  XA): at N=30 two iterations vs oracle.gn_general (dense KKT, row by row --
-  too slow at N=200), same tolerance; at the full N=200 shape size-independent properties: all
+* C5 as SURVEY.md §8(d) defines it (8 receivers, n = 40, d = 8040 at N = 200; mixed
+  pseudorange rows per receiver + range_3d between adjacent receivers): at N = 10
+  (d = 440) two iterations vs oracle.gn_general (dense, row by row), same tolerance;
+  at the full shape, properties (below) and batch chunking bit-identical to one launch.
+* C5s (the reference's own multi-receiver.py structure, n = 8 + the extra variable XA;
+  mixed rows: pseudorange, pseudorange rate, 2-D range to XA): at N=30 two iterations
+  vs oracle.gn_general, same tolerance; at the full N=200 shape size-independent properties: all
   trajectories converge (the GN step itself, max|delta| <= tol (1 + max|X|), is the
   stationarity check), the cost ends below its start (undamped GN need not decrease
   it monotonically), XA[2] (no row depends on it) is held bit-exactly, and the
@@ -49,14 +53,35 @@ def test_c4_full_shape_matches_oracle():
     tl.check("C4 cost", np.abs(cost - cr).max(), tl.FLOOR_MULT * fc + 1e-10 * np.abs(cr).max())
 
 
+def test_c3_full_shape_real_geometry_matches_oracle():
+    """C3 as SURVEY §8(d) specifies it: the satellite epochs of data/gnss_stationary's log
+    (tests/golden/gnss_stationary_c3.npz; 57 empty slots masked with R = 0)."""
+    w = configs.make_c3(B=2)
+    s = solver.from_workload(w)
+    assert s.large_system and (w.Rw == 0).any()
+    X, cost, iters, status = _np(s.solve(w.X_init, w.U, w.Y, w.PAR, max_iter=3, tol=0.0))
+    pb = gn.Problem(w.N, w.T, w.n, w.m, w.dyn, w.meas, w.cpm.D, (w.T / 2) * w.cpm.w,
+                    w.cpm.lagrange_matrix(w.t_meas), w.Qw, w.Rw, meas_static=w.meas_static)
+    U = np.broadcast_to(w.U, (w.B,) + w.U.shape[1:])
+    PAR = np.broadcast_to(w.PAR, (w.B,) + w.PAR.shape[1:])
+    run = lambda Y, pt=None: gn.gauss_newton(pb, w.X_init, U, Y, PAR, max_iter=3, tol=0.0, perturb=pt)  # noqa: E731
+    Xr, cr, ir, sr = run(w.Y)
+    fx, fc = tl.floor(lambda Y, pt: run(Y, pt)[:2], w.Y)
+    assert iters.tolist() == ir.tolist() == [3, 3] and status.tolist() == sr.tolist()
+    b = tl.bound(fx, Xr)
+    tl.check("C3 X", np.abs(X - Xr).max(), b, " m")
+    assert b < 1e-4
+    tl.check("C3 cost", np.abs(cost - cr).max(), tl.FLOOR_MULT * fc + 1e-10 * np.abs(cr).max())
+
+
 def _c5_solver(w):
     s = solver.from_workload(w)
     assert s.large_system and s.n_extra == 3
     return s
 
 
-def test_c5_reduced_matches_kkt_oracle():
-    w = configs.make_c5(B=2, N=30)
+def test_c5s_reduced_matches_kkt_oracle():
+    w = configs.make_c5_small(B=2, N=30)
     s = _c5_solver(w)
     X, cost, iters, st, Z = _np(s.solve(w.X_init, None, w.Y, w.PAR, max_iter=2, tol=0.0, Z0=w.Z_init))
     pb = gg.GeneralProblem(w.N, w.T, w.n, w.m, w.dyn, "mixed", w.cpm.D, (w.T / 2) * w.cpm.w,
@@ -73,8 +98,8 @@ def test_c5_reduced_matches_kkt_oracle():
     tl.check("C5 cost", np.abs(cost - cr).max(), tl.FLOOR_MULT * fc + 1e-10 * np.abs(cr).max())
 
 
-def test_c5_full_shape_properties():
-    w = configs.make_c5(B=4)
+def test_c5s_full_shape_properties():
+    w = configs.make_c5_small(B=4)
     s = _c5_solver(w)
     X, c0, iters, st, Z = _np(s.solve(w.X_init, None, w.Y, w.PAR, max_iter=0, tol=0.0, Z0=w.Z_init))
     assert np.all(np.isfinite(c0)) and iters.tolist() == [0] * w.B
@@ -84,3 +109,53 @@ def test_c5_full_shape_properties():
     assert np.array_equal(Z[:, 2], w.Z_init[:, 2])          # XA[2] enters no row: held
     assert np.abs(X[:, :, :3] - w.X_true[:, :, :3]).max() < 10.0  # sigma_pr = 10 m
     assert np.abs(Z[:, :2] - w.Z_true[:, :2]).max() < 3.0
+
+
+def _c5_pb(w):
+    return gg.GeneralProblem(w.N, w.T, w.n, w.m, w.dyn, "mixed", w.cpm.D, (w.T / 2) * w.cpm.w,
+                             w.cpm.lagrange_matrix(w.t_meas), w.Qw, w.Rw)
+
+
+def test_c5_eight_receivers_reduced_matches_oracle():
+    """SURVEY §8(d) C5 structure (n = 40) at N = 10 (d = 440) vs the dense oracle."""
+    w = configs.make_c5(B=2, N=10)
+    s = solver.from_workload(w)
+    assert s.large_system and s.n == 40 and s.m == 24
+    X, cost, iters, st = _np(s.solve(w.X_init, w.U, w.Y, w.PAR, max_iter=2, tol=0.0))
+    pb = _c5_pb(w)
+    run = lambda Y, pt=None: gg.gauss_newton_general(pb, w.X_init, None, w.U, Y, w.PAR, None,  # noqa: E731
+                                                     max_iter=2, tol=0.0, perturb=pt)
+    Xr, _, cr, ir, sr = run(w.Y)
+    fx, fc = tl.floor(lambda Y, pt: (lambda r: (r[0], r[2]))(run(Y, pt)), w.Y)
+    assert iters.tolist() == ir.tolist() == [2, 2] and st.tolist() == sr.tolist()
+    b = tl.bound(fx, Xr)
+    tl.check("C5 (n=40, N=10) X", np.abs(X - Xr).max(), b, " m")
+    assert b < 1e-4
+    tl.check("C5 cost", np.abs(cost - cr).max(), tl.FLOOR_MULT * fc + 1e-10 * np.abs(cr).max())
+
+
+def test_c5_eight_receivers_full_shape():
+    """d = 8040 (N = 200, n = 40): every trajectory converges, the cost drops, the
+    receivers are recovered to the noise level (sigma_pr = 1 m, 96 pseudoranges an
+    epoch), and streaming the batch through a 1-trajectory workspace (chunking: C5's
+    2048 trajectories per GPU x 0.28 GB do not fit 288 GB at once) is bit-identical."""
+    w = configs.make_c5(B=3)
+    s = solver.from_workload(w)
+    assert s.dp == 40 * 208 and s.large_system
+    X, c0, iters, st = _np(s.solve(w.X_init, w.U, w.Y, w.PAR, max_iter=0, tol=0.0))
+    X, cost, iters, st = _np(s.solve(w.X_init, w.U, w.Y, w.PAR, max_iter=30, tol=1e-9))
+    print("C5 d=8040: iterations", iters.tolist(), "status", st.tolist())
+    assert st.tolist() == [0] * w.B and np.all(cost < c0)
+    pos = [c for r in range(8) for c in (5 * r, 5 * r + 1, 5 * r + 2)]
+    err = np.abs(X[:, :, pos] - w.X_true[:, :, pos]).max()
+    print(f"C5 d=8040: max position error {err:.2f} m")
+    assert err < 3.0
+    a = _np(s.solve(w.X_init, w.U, w.Y, w.PAR, max_iter=2, tol=0.0))
+    per = s.lib.mhe_workspace_bytes(s.dims, 1)
+    s.ws_budget = per          # one trajectory per launch
+    try:
+        b = _np(s.solve(w.X_init, w.U, w.Y, w.PAR, max_iter=2, tol=0.0))
+    finally:
+        s.ws_budget = None
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)

@@ -3,10 +3,11 @@
     python tools/bench_big.py [C3|C4|C5] [B] [iters]
 
 GN collocation-point updates/s = B * P * iters / device time (HIP events around one
-mhe_gn_solve_ws call with tol = 0, inputs resident), and the algorithmic FP64 rate
-by SURVEY.md §8(d)'s count per trajectory-iteration:
-    F = d^3/3 + 2 d^2 + E P^2 nnz(G_e) + 2 P^2 n^2 + 4 P n^3
-(nnz(G_e): state components the epoch's rows touch, squared).
+mhe_solve call with tol = 0, inputs resident; a batch whose workspace exceeds the free
+HBM is streamed through one workspace in chunks), and the algorithmic FP64 rate by
+SURVEY.md §8(d)'s count per trajectory-iteration:
+    F = d^3/3 + 2 d^2 + sum_e P^2 nnz(G_e) + 2 P^2 n^2 + 4 P n^3
+(nnz(G_e): the component pairs the epoch's unmasked rows couple).
 """
 import json
 import os
@@ -26,8 +27,30 @@ s = solver.from_workload(w)
 P, n = w.P, w.n
 d = P * n
 E = np.unique(w.t_meas).shape[0]
-touched = {"C2": 2, "C3": 4, "C4": 4, "C5": 8}[cfg]
-F = d ** 3 / 3 + 2 * d * d + E * P * P * touched ** 2 + 2 * P * P * n * n + 4 * P * n ** 3
+
+
+def nnz_g_sum():
+    """sum over epochs of nnz(G_e): the (a, b) component pairs some unmasked row of the
+    epoch couples (pseudorange: x, y, z, b; mixed rows: the row's state indices)."""
+    t, Rw = w.t_meas, np.asarray(w.Rw).reshape(len(w.t_meas), -1)
+    total = 0
+    for te in np.unique(t):
+        pairs = set()
+        for i in np.nonzero(t == te)[0]:
+            if not np.any(Rw[i]):
+                continue
+            if w.meas == "mixed":
+                ids = [int(v) for v in w.PAR[0, i, 1:8] if 0 <= v < n]
+            elif w.meas == "pseudorange":
+                ids = list(w.meas_static["idx"])
+            else:
+                ids = list(range(n))
+            pairs |= {(a, b) for a in ids for b in ids}
+        total += len(pairs)
+    return total
+
+
+F = d ** 3 / 3 + 2 * d * d + nnz_g_sum() * P * P + 2 * P * P * n * n + 4 * P * n ** 3
 Z0 = getattr(w, "Z_init", None)
 
 
@@ -48,6 +71,6 @@ res = {"config": cfg, "workload": w.name, "B": B, "iters": it, "d": d, "P": P, "
        "ms_per_iter": dt / it * 1e3, "pt_updates_per_s": B * P * it / dt,
        "mflop_per_traj_iter": F / 1e6, "achieved_tflops": F * B * it / dt / 1e12,
        "frac_fp64_peak": F * B * it / dt / 1e12 / 78.6,
-       "workspace_gib": s.lib.mhe_workspace_bytes(s.dims, B) / 2 ** 30,
+       "workspace_gib": s.lib.mhe_workspace_bytes(s.dims, B) / 2 ** 30, "chunk": s._chunk(B),
        "status": sorted(set(st.tolist()))}
 print(json.dumps(res))
