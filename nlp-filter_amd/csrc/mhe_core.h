@@ -34,14 +34,20 @@ namespace mhe {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
-constexpr int NW = 8;              // waves per workgroup (one trajectory)
+// waves per workgroup (one trajectory).  -DMHE_NW=16 builds the one-workgroup-per-CU
+// shape (5 slots per wave, 99 VGPRs, no scratch; bitwise-identical iterates) for A/B
+// runs -- measured 5 % slower at B = 128 and 256, 38 % at 1024
+#ifndef MHE_NW
+#define MHE_NW 8
+#endif
+constexpr int NW = MHE_NW;
 constexpr int NTHREADS = NW * 64;
 constexpr int MAX_NT = 13;         // padded system <= 208 (register-resident path)
 // The NT(NT-1)/2 off-diagonal tiles live in MFMA accumulator registers (20
 // slots per wave at NT = 13, 160 VGPRs); the NT diagonal tiles live in LDS.
 // Holding all 91 tiles in registers (23 slots) left too few registers for the
 // rest of the kernel and the allocator spilled tiles to scratch.
-constexpr int MAX_SLOTS = (MAX_NT * (MAX_NT - 1) / 2 + NW - 1) / NW;  // 20
+constexpr int MAX_SLOTS = (MAX_NT * (MAX_NT - 1) / 2 + NW - 1) / NW;  // 10 at 8 waves
 
 enum Mode { MODE_SOLVE = 0, MODE_ASSEMBLE = 1, MODE_LINSOLVE = 2 };
 
@@ -80,7 +86,7 @@ __host__ __device__ inline ConstLayout const_layout(int P, int M, int n, int p, 
 }
 
 struct SmemLayout {  // offsets in doubles
-  int Xs, Vs, FtV, Es, FtE, GE, G, LAM, BV, YV, PB, DT, RED, ROWM, UN, SIM, XO, ACT, GV, total;
+  int Xs, Vs, FtV, Es, FtE, GE, G, LAM, BV, YV, PB, DT, RED, ROWM, UN, XO, ACT, GV, total;
 };
 
 __host__ __device__ inline int rnd2(int x) { return (x + 1) & ~1; }  // keep 16-B alignment
@@ -113,7 +119,6 @@ __host__ __device__ inline SmemLayout smem_layout(int P, int M, int n, int NT, b
   S.RED = o;  o += 4 * NW + 8;
   S.ROWM = o; o += NW * 8;              // per wave, per block row I: bit mask of its slots (I, J)
   S.UN = o;   o += UNITS;               // identity rows for the panel (unit_row)
-  S.SIM = o;  o += 8;                   // int[NW]: SIMD of each wave; int[NW]: the panel-done flag (MHE_DEFER_SIMD)
   // bounded problems only (projected Newton, k_gn<..., BOUNDED>): the iterate the
   // line search starts from, and the epsilon-active set (one int per unknown)
   S.XO = o;   o += bounded ? rnd2(P * n) : 0;
@@ -1030,25 +1035,6 @@ __device__ __forceinline__ void load_tiles(const GnArgs& a, const SmemLayout& SL
     }
 }
 
-// f64 MFMA and VALU do not co-issue on a gfx950 SIMD: while the panel
-// wave runs its ~500-instruction VALU sweep, MFMAs issued by a wave sharing its SIMD
-// stall it.  With MHE_DEFER_SIMD the waves of this workgroup on the panel wave's SIMD
-// start their trailing-update work only once the panel is done (an LDS flag).  Each
-// wave's SIMD comes from HW_REG_HW_ID (SIMD_ID, bits 5:4).
-#ifndef MHE_DEFER_SIMD
-#define MHE_DEFER_SIMD 0
-#endif
-__device__ __forceinline__ int wave_simd_id() {
-  // s_getreg_b32 HW_REG_HW_ID (id 4), offset 4, size 2
-  return __builtin_amdgcn_s_getreg((4 << 0) | (4 << 6) | ((2 - 1) << 11));
-}
-__device__ __forceinline__ void init_simd_ids(double* sim, int wave, int lane) {
-  if (lane == 0) {
-    ((int*)sim)[wave] = wave_simd_id();
-    ((int*)sim)[NW] = -2;  // panel-done flag: the step whose panel is complete
-  }
-}
-
 // LDS ordering between lanes of ONE wave: LDS operations of a wave execute in
 // order, so a compiler-level fence plus a wait on the wave's own stores suffices.
 __device__ __forceinline__ void wave_lds_sync() {
@@ -1157,7 +1143,9 @@ __device__ __forceinline__ double rsqrt_pivot(double x) {
 // stride LIS).  The right-hand side is NOT carried here: y_k = L_kk^-1 b_k is formed
 // later by another wave (off this critical chain).
 // Returns true if a pivot was not positive and finite (wave-uniform; tested on the
-// high word in scalar ALU: pivots below 2^-1022 count as not positive).
+// high word in scalar ALU: a pivot passes when its high word is in [1, 0x7FEFFFFF],
+// i.e. positive, finite and >= 2^-1042 -- the larger subnormals pass, zero, the
+// smallest subnormals, negatives, inf and NaN are flagged).
 __device__ __forceinline__ bool panel(double* DTk, const double* UN, int lane) {
   const int i = lane & 15;
   const bool erow = (lane >= 16 && lane < 32);
@@ -1173,7 +1161,7 @@ __device__ __forceinline__ bool panel(double* DTk, const double* UN, int lane) {
 #pragma unroll
   for (int c = 0; c < 16; ++c) {
     const double piv = readlane_d(v[c], c);
-    bad |= (unsigned)__double2hiint(piv) - 1u >= 0x7FEFFFFFu;  // not in [2^-1022, inf)
+    bad |= (unsigned)__double2hiint(piv) - 1u >= 0x7FEFFFFFu;  // high word not in [1, 0x7FEFFFFF]
     double q = v[c] * rsqrt_pivot(piv);
     v[c] = q;
     if (c < 15) {
@@ -1279,16 +1267,7 @@ __device__ __forceinline__ bool factor_forward(const GnArgs& a, const SmemLayout
       }
       if (!KO(3)) bad |= panel(DTn, sm + SL.UN, lane_o);
       __builtin_amdgcn_s_setprio(0);
-      if (MHE_DEFER_SIMD && lane_o == 0)
-        __hip_atomic_store(((int*)(sm + SL.SIM)) + NW, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     } else if (k >= 0 && !KO(4)) {
-      if (MHE_DEFER_SIMD && ((const int*)(sm + SL.SIM))[wave_o] == ((const int*)(sm + SL.SIM))[pw]) {
-        // same SIMD as the panel wave: keep the MFMA pipe free until the panel is done
-        // (bounded: a wave always leaves the spin, whatever the flag says)
-        for (int spin = 0; spin < (1 << 16) &&
-             __hip_atomic_load(((int*)(sm + SL.SIM)) + NW, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != k; ++spin)
-          __builtin_amdgcn_s_sleep(1);
-      }
       // b_b -= U_kb^T y_k for b >= k + 1: one output per lane of the other waves
       const int vt = ((wave_o - pw - 1 + NW) % NW) * 64 + lane_o;
       const int bq = k + 1 + (vt >> 4), c = vt & 15;
@@ -1500,7 +1479,7 @@ __device__ __forceinline__ int opaque_s(int x) {
 #define FSL smem_layout(opaque_s(a.P), opaque_s(a.M), n, opaque_s(a.NT), !MEAS::LINEAR)
 
 template <class DYN, class MEAS, int SLOTS, int mode, bool HUBER = false>
-__global__ __launch_bounds__(NTHREADS, NW / 2) void k_gn(GnArgs a) {  // 2nd arg: min waves per SIMD (2 WGs per CU)
+__global__ __launch_bounds__(NTHREADS, 4) void k_gn(GnArgs a) {  // 2nd arg: min waves per SIMD (8 waves: 2 WGs per CU)
   constexpr int n = DYN::n;
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const ConstLayout CL = const_layout(a.P, a.M, n, MEAS::p, a.NT);
@@ -1513,7 +1492,6 @@ __global__ __launch_bounds__(NTHREADS, NW / 2) void k_gn(GnArgs a) {  // 2nd arg
   double* Xs = sm + SL.Xs;
   if (threadIdx.x == 0) *(int*)(sm + SL.RED + 4 * NW) = 0;  // NOT_SPD flag
   init_units(sm + SL.UN);
-  init_simd_ids(sm + SL.SIM, wave, lane);
   double* DV = sm + SL.YV;  // delta after backward()
   double* RED = sm + SL.RED;
   d4 acc[SLOTS];
@@ -1696,7 +1674,7 @@ __device__ __forceinline__ double prior_cost(const GnArgs& a, const double* Pw, 
 #define FSLB smem_layout(opaque_s(a.P), opaque_s(a.M), n, opaque_s(a.NT), !MEAS::LINEAR, true)
 
 template <class DYN, class MEAS, int SLOTS, bool HUBER = false>
-__global__ __launch_bounds__(NTHREADS, NW / 2) void k_gn_bounded(GnArgs a) {
+__global__ __launch_bounds__(NTHREADS, 4) void k_gn_bounded(GnArgs a) {
   constexpr int n = DYN::n;
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const SmemLayout SL = smem_layout(a.P, a.M, n, a.NT, !MEAS::LINEAR, true);
@@ -1714,7 +1692,6 @@ __global__ __launch_bounds__(NTHREADS, NW / 2) void k_gn_bounded(GnArgs a) {
   double* RED = sm + SL.RED;
   if (threadIdx.x == 0) *(int*)(sm + SL.RED + 4 * NW) = 0;  // NOT_SPD flag
   init_units(sm + SL.UN);
-  init_simd_ids(sm + SL.SIM, wave, lane);
   d4 acc[SLOTS];
 #pragma unroll
   for (int s = 0; s < SLOTS; ++s) acc[s] = d4{0.0, 0.0, 0.0, 0.0};

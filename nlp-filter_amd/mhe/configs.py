@@ -303,7 +303,7 @@ def make_c5_small(B=2048, seed=4, N=200, epochs=None, n_sat=12):
                     X_true=xt, Z_true=xa, cpm=cpm)
 
 
-def make_c5(B=2048, seed=4, N=200, R=8, r_pr=1.0, r_range=0.01, spacing=5.0):
+def make_c5(B=2048, seed=4, N=200, R=8, r_pr=1.0, r_range=0.01, spacing=0.5 * 91.44):
     """C5 as SURVEY.md §8(d) defines it: 8 receivers, each the per-receiver block of
     gnss_two_receiver [x, y, z, b, alpha] (nlp/dynamics.py:98-115) -> n = 40, m = 24
     (each receiver's velocity as its control, as gnss-multi-receiver.py:156-165 feeds
@@ -312,7 +312,11 @@ def make_c5(B=2048, seed=4, N=200, R=8, r_pr=1.0, r_range=0.01, spacing=5.0):
     multi_receiver_range_3d row between each adjacent pair (nlp/measurements.py:39-54),
     mixed rows (include/mhe.h).  N = 200, T = 200 s, 201 epochs x (96 + 7) rows, d = 8040.
     Weights as gnss-multi-receiver.py:43-48 (Q per receiver block, r_pr = 1 (B's),
-    r_range = 0.01, dt = 1 s).  Receivers in a line `spacing` m apart, moving together."""
+    r_range = 0.01, dt = 1 s).  Receivers in a line `spacing` m apart, moving together
+    (default the script's 50-yard baseline, gnss-multi-receiver.py:68).  Gauss-Newton's
+    local rate here is set by the range rows' dropped curvature R e (I - u u^T) / |d|:
+    at a 5 m baseline it exceeds the Gauss-Newton curvature of the receivers' relative
+    position and the iteration oscillates (IPOPT's exact Hessian would not)."""
     T = float(N)
     epochs = N + 1
     rng = np.random.default_rng(seed)

@@ -113,11 +113,11 @@ def test_bounds_iterates_match_oracle_fixed_count_large_system_path():
 
 
 def _backtracking_case():
-    """A far start (2 X_init + 2) under the same bounds: the oracle's Armijo search
-    halves the step several times (the line search must use the gradient
+    """A far start (4 X_init) under the same bounds: the oracle's Armijo search
+    halves the step several times (6 of the 8 x B steps, one of them twice) (the line search must use the gradient
     at the iterate, not the forward-substituted right-hand side)."""
     w, bounds, pb = _bounds_case()
-    X0 = 2.0 * w.X_init + 2.0
+    X0 = 4.0 * w.X_init
     trace = []
     Xr, cr, ir, sr = gn.gauss_newton(pb, X0, _U(w), w.Y, max_iter=8, tol=0.0, trace=trace)
     assert sum(a < 1.0 for _, _, a in trace) >= 4, "the case should backtrack"
