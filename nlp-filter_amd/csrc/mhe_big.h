@@ -701,9 +701,14 @@ __global__ __launch_bounds__(256, 4) void k_big_assemble(BigArgs a) {
 // ------------------------------------------------------------ factor + solve
 // Blocked right-looking Cholesky over super-blocks of BIG_KB tile columns
 // (nb = 16 BIG_KB).  Per super-block:
-//   panel phase   the block column, 16 columns at a time: single-wave diagonal
-//                 panel (L_kk^-T, y_k), MFMA TRSM of the tiles below, updates
-//                 restricted to the block column's own tiles;
+//   diagonal block  the BIG_KB x BIG_KB tiles of the block's own rows, 16 columns at
+//                 a time: single-wave diagonal panel (L_kk^-T, y_k), in-block updates
+//                 left-looking from LDS, MFMA TRSM -- two workgroup barriers per k;
+//   rows below    every row I >= block end independently (one wave per row, no
+//                 barriers): its BIG_KB tiles A_Ik are read once, the in-block
+//                 updates and the TRSMs run from registers (the row's L_Ik' stay in
+//                 VGPRs, L_kk' and L_kk^-1 come from LDS), L_Ik written once, and
+//                 b_I -= L_Ik y_k;
 //   trailing      A_IJ -= sum_{k in block} L_Ik L_Jk^T for all J >= block end:
 //                 K = nb per tile visit, so every trailing tile is read and
 //                 written once per nb columns instead of once per 16 (the 16-wide
@@ -722,8 +727,12 @@ constexpr int BIG_WIDE_NT = 128;
 #define MHE_BIG_KO 0  // knock-out mask for timing probes only (tools/ko_big.sh): 1 trailing, 2 in-block, 4 TRSM
 #endif
 constexpr int BIG_LB_TILES = BIG_KB * (BIG_KB - 1) / 2;
-__host__ __device__ constexpr int big_slab_tiles(int JB) { return JB * BIG_KB > BIG_LB_TILES ? JB * BIG_KB : BIG_LB_TILES; }
-__host__ __device__ constexpr int big_chol_lds(int JB) { return DTS + BIG_NW * 16 + 16 + 2 + UNITS + big_slab_tiles(JB) * 256; }  // doubles
+// the LJ region: the trailing slab, or (panel phase) the in-block L tiles LB and the
+// block's L_kk^-T matrices LTs
+__host__ __device__ constexpr int big_slab_doubles(int JB) {
+  return JB * BIG_KB * 256 > BIG_LB_TILES * 256 + BIG_KB * DTS ? JB * BIG_KB * 256 : BIG_LB_TILES * 256 + BIG_KB * DTS;
+}
+__host__ __device__ constexpr int big_chol_lds(int JB) { return DTS + BIG_NW * 16 + 16 + 2 + UNITS + big_slab_doubles(JB); }  // doubles
 
 template <int BIG_JB>
 __global__ __launch_bounds__(BIG_NTHREADS, BIG_JB == 8 ? 2 : 4) void k_big_chol(BigArgs a) {
@@ -748,12 +757,13 @@ __global__ __launch_bounds__(BIG_NTHREADS, BIG_JB == 8 ? 2 : 4) void k_big_chol(
   init_units(UN);
   for (int k0 = 0; k0 < NT; k0 += BIG_KB) {
     const int kend = min(k0 + BIG_KB, NT);
-    // ---- panel phase, left-looking inside the block column: at step k every tile
-    // (I, k), I >= k, gets all of its in-block updates in ONE pass (K = 16 (k - k0),
+    // ---- diagonal block, left-looking inside the block column: at step k every tile
+    // (I, k), k <= I < kend, gets all of its in-block updates in ONE pass (K = 16 (k - k0),
     // L_kk' operands from LDS), then the TRSM.  Two workgroup barriers per k.
     // LB (= the LJ region, free until the trailing phase): L_Ik' for k0 <= k' < I < kend, packed
-    // strictly-lower: slot (I - k0)(I - k0 - 1)/2 + (k' - k0).
+    // strictly-lower: slot (I - k0)(I - k0 - 1)/2 + (k' - k0); LTs: L_kk^-T of the block's k.
     double* LB = LJ;
+    double* LTs = LJ + BIG_LB_TILES * 256;
     for (int k = k0; k < kend; ++k) {
       const int nk = k - k0;
       if (wave == 0) {
@@ -777,17 +787,20 @@ __global__ __launch_bounds__(BIG_NTHREADS, BIG_JB == 8 ? 2 : 4) void k_big_chol(
         if (bad && lane == 0) *flag = 1;
         wave_lds_sync();
         block_fwd(DT, BV + 16 * k, YV + 16 * k, lane);  // y_k = L_kk^-1 b_k
-        for (int e = lane; e < DTS; e += 64) LTg[(size_t)k * DTS + e] = DT[e];
+        for (int e = lane; e < DTS; e += 64) {
+          LTg[(size_t)k * DTS + e] = DT[e];
+          LTs[nk * DTS + e] = DT[e];
+        }
       } else {
-        // rows I > k: c' = A_Ik^T - sum_k' L_kk' L_Ik'^T, stored k-major in place (= A_Ik^T row-major)
-        for (int I = k + wave; I < NT; I += BIG_NW - 1) {
+        // block rows k < I < kend: c' = A_Ik^T - sum_k' L_kk' L_Ik'^T, stored k-major in place (= A_Ik^T row-major)
+        for (int I = k + wave; I < kend; I += BIG_NW - 1) {
           double* Ak = H + (size_t)big_tile_index(I, k, NT) * 256;
           d4 c;
 #pragma unroll
           for (int r = 0; r < 4; ++r) c[r] = Ak[(lane & 15) * 16 + 4 * r + (lane >> 4)];
           for (int kk = 0; kk < nk && !(MHE_BIG_KO & 2); ++kk) {
             const double* Lk = LB + (nk * (nk - 1) / 2 + kk) * 256;
-            const double* LI = H + (size_t)big_tile_index(I, k0 + kk, NT) * 256;
+            const double* LI = LB + ((I - k0) * (I - k0 - 1) / 2 + kk) * 256;
 #pragma unroll
             for (int r = 0; r < 4; ++r)
               c = __builtin_amdgcn_mfma_f64_16x16x4f64(Lk[64 * r + lane], LI[64 * r + lane], c, 0, 0, MFMA_NEG_A);
@@ -798,10 +811,10 @@ __global__ __launch_bounds__(BIG_NTHREADS, BIG_JB == 8 ? 2 : 4) void k_big_chol(
       }
       __syncthreads();
       if (*flag) break;
-      // TRSM: L_Ik^T = L_kk^-1 A_Ik^T (k-major result), b_I -= L_Ik y_k; in-block L_Ik also to LB
+      // TRSM: L_Ik^T = L_kk^-1 A_Ik^T (k-major result) for the block rows, b_I -= L_Ik y_k; L_Ik also to LB
       const double yk = YV[16 * k + (lane >> 4)], yk1 = YV[16 * k + 4 + (lane >> 4)],
                    yk2 = YV[16 * k + 8 + (lane >> 4)], yk3 = YV[16 * k + 12 + (lane >> 4)];
-      for (int I = k + 1 + wave; I < NT && !(MHE_BIG_KO & 4); I += BIG_NW) {
+      for (int I = k + 1 + wave; I < kend && !(MHE_BIG_KO & 4); I += BIG_NW) {
         double* Ak = H + (size_t)big_tile_index(I, k, NT) * 256;
         double av[4], bv[4];
 #pragma unroll
@@ -813,11 +826,11 @@ __global__ __launch_bounds__(BIG_NTHREADS, BIG_JB == 8 ? 2 : 4) void k_big_chol(
 #pragma unroll
         for (int r = 0; r < 4; ++r) u = __builtin_amdgcn_mfma_f64_16x16x4f64(av[r], bv[r], u, 0, 0, 0);
         // u[r] = L_Ik[lane & 15][(lane >> 4) + 4 r]
-        double* LBs = (I < kend) ? LB + ((I - k0) * (I - k0 - 1) / 2 + nk) * 256 : nullptr;
+        double* LBs = LB + ((I - k0) * (I - k0 - 1) / 2 + nk) * 256;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           Ak[64 * r + lane] = u[r];
-          if (LBs) LBs[64 * r + lane] = u[r];
+          LBs[64 * r + lane] = u[r];
         }
         double s = u[0] * yk + u[1] * yk1 + u[2] * yk2 + u[3] * yk3;
         s += __shfl_xor(s, 16);
@@ -827,8 +840,41 @@ __global__ __launch_bounds__(BIG_NTHREADS, BIG_JB == 8 ? 2 : 4) void k_big_chol(
       __syncthreads();
     }
     if (*flag) break;
-    // ---- trailing update with K = (kend - k0) tiles
+    // ---- rows below the block, one wave per row: the same operations per element as
+    // the diagonal block's (in-block updates in k' order, TRSM, b_I update in k order),
+    // without barriers; the row's L_Ik' are re-read right after this wave wrote them
+    // (L2 hits: the old form re-read them after a sweep over every row)
     const int kb = kend - k0;
+    for (int I = kend + wave; I < NT; I += BIG_NW) {
+      for (int kk = 0; kk < kb; ++kk) {
+        double* Ak = H + (size_t)big_tile_index(I, k0 + kk, NT) * 256;
+        d4 c;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) c[r] = Ak[(lane & 15) * 16 + 4 * r + (lane >> 4)];
+        for (int kp = 0; kp < kk && !(MHE_BIG_KO & 2); ++kp) {
+          const double* Lk = LB + (kk * (kk - 1) / 2 + kp) * 256;
+          const double* LI = H + (size_t)big_tile_index(I, k0 + kp, NT) * 256;
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            c = __builtin_amdgcn_mfma_f64_16x16x4f64(Lk[64 * r + lane], LI[64 * r + lane], c, 0, 0, MFMA_NEG_A);
+        }
+        const double* LT = LTs + kk * DTS;
+        d4 t = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          t = __builtin_amdgcn_mfma_f64_16x16x4f64(LT[(4 * r + (lane >> 4)) * LIS + (lane & 15)], c[r], t, 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Ak[64 * r + lane] = t[r];
+        const int k = k0 + kk;
+        double s = t[0] * YV[16 * k + (lane >> 4)] + t[1] * YV[16 * k + 4 + (lane >> 4)] +
+                   t[2] * YV[16 * k + 8 + (lane >> 4)] + t[3] * YV[16 * k + 12 + (lane >> 4)];
+        s += __shfl_xor(s, 16);
+        s += __shfl_xor(s, 32);
+        if (lane < 16) BV[16 * I + lane] -= s;
+      }
+    }
+    __syncthreads();
+    // ---- trailing update with K = (kend - k0) tiles
     for (int J0 = kend; J0 < NT && !(MHE_BIG_KO & 1); J0 += BIG_JB) {
       const int jb = min(BIG_JB, NT - J0);
       // stage L_Jk (jb x kb tiles) into LDS
