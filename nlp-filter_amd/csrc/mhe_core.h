@@ -1346,6 +1346,7 @@ __device__ __forceinline__ double rows4_sum(double v) {
 }
 
 __device__ __forceinline__ void block_fwd(const double* LT, const double* b, double* y, int lane) {
+  asm volatile("" : "+v"(lane));  // derive c, g here: a kernel-wide copy of them is what spilled
   const int c = lane & 15, g = lane >> 4;
   const double2 b01 = *(const double2*)(b + 4 * g);
   const double2 b23 = *(const double2*)(b + 4 * g + 2);
@@ -1361,6 +1362,7 @@ __device__ __forceinline__ void block_fwd(const double* LT, const double* b, dou
 // delta_k = L_kk^-T y_k, in place, by one whole wave: lane (c, g = l >> 4) sums
 // the four terms q = 4g..4g+3 of row c of L^-T, rows4_sum completes the dot.
 __device__ __forceinline__ void block_back(const double* LT, double* yv, int lane) {
+  asm volatile("" : "+v"(lane));  // as block_fwd: no kernel-wide copy of c, g
   const int c = lane & 15, g = lane >> 4;
   const double2 y01 = *(const double2*)(yv + 4 * g);
   const double2 y23 = *(const double2*)(yv + 4 * g + 2);
