@@ -722,7 +722,10 @@ constexpr int BIG_KB = 8;      // tile columns per super-block
 // 1 / JB.  JB = 8 (128 KB slab, one workgroup per CU) for wide systems (NT >=
 // BIG_WIDE_NT, C4: HBM-bound there), JB = 4 (64 KB, two workgroups per CU, whose
 // overlap the latency-bound panel phase of narrower systems needs) otherwise.
-constexpr int BIG_WIDE_NT = 128;
+#ifndef MHE_BIG_WIDE_NT
+#define MHE_BIG_WIDE_NT 128
+#endif
+constexpr int BIG_WIDE_NT = MHE_BIG_WIDE_NT;
 #ifndef MHE_BIG_KO
 #define MHE_BIG_KO 0  // knock-out mask for timing probes only (tools/ko_big.sh): 1 trailing, 2 in-block, 4 TRSM
 #endif

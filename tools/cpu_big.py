@@ -33,15 +33,17 @@ def problem(w):
                       w.cpm.lagrange_matrix(w.t_meas), w.Qw, w.Rw, Pw=w.Pw, meas_static=w.meas_static)
 
 
-def one_config(cfg, Bs, reps):
-    w = configs.CONFIGS[cfg](B=Bs)
+def one_config(cfg, Bs, reps, N=None):
+    w = configs.CONFIGS[cfg](B=Bs, **({} if N is None else {"N": N}))
     U = None if w.U is None else np.broadcast_to(w.U, (w.B,) + w.U.shape[1:])
     PAR = None if w.PAR is None else np.broadcast_to(w.PAR, (w.B,) + w.PAR.shape[1:])
-    if getattr(w, "Z_init", None) is not None:  # C5: extra variables z (XA) -> dense KKT step
+    if w.meas == "mixed":  # C5: mixed rows (+ extra variables z) -> oracle.gn_general's dense KKT step
         from oracle import gn_general as gg
+        Z0 = getattr(w, "Z_init", None)
         gp = gg.GeneralProblem(w.N, w.T, w.n, w.m, w.dyn, "mixed", w.cpm.D, (w.T / 2) * w.cpm.w,
-                               w.cpm.lagrange_matrix(w.t_meas), w.Qw, w.Rw, n_extra=w.Z_init.shape[-1])
-        step = lambda X: gg.gauss_newton_general(gp, X, w.Z_init, None, w.Y, w.PAR, None,  # noqa: E731
+                               w.cpm.lagrange_matrix(w.t_meas), w.Qw, w.Rw,
+                               **({} if Z0 is None else {"n_extra": Z0.shape[-1]}))
+        step = lambda X: gg.gauss_newton_general(gp, X, Z0, U, w.Y, w.PAR, None,  # noqa: E731
                                                  max_iter=1, tol=0.0)
     else:
         pb = problem(w)
@@ -53,16 +55,18 @@ def one_config(cfg, Bs, reps):
     dt = (time.perf_counter() - t0) / reps
     return {"config": cfg, "workload": w.name, "subset_B": Bs, "d": w.P * w.n, "P": w.P,
             "s_per_traj_iter": dt / Bs, "pt_updates_per_s": Bs * w.P / dt,
-            "note": f"CPU subset of {Bs} trajectories, {reps} timed GN iteration(s) after 1 warm-up"}
+            "note": f"CPU subset of {Bs} trajectories, {reps} timed GN iteration(s) after 1 warm-up"
+                    + ("" if N is None else f"; REDUCED horizon N = {N} (not the config's shape)")}
 
 
 def main():
     args = sys.argv[1:]
     cfgs = [a for a in args if a in DEFAULT_SUBSET] or ["C3", "C4"]
+    n_red = int(args[args.index("--N") + 1]) if "--N" in args else None  # reduced horizon (C5: labelled)
     sub = int(args[args.index("--subset") + 1]) if "--subset" in args else None
     threads = len(os.sched_getaffinity(0))
     for cfg in cfgs:
-        r = one_config(cfg, sub or DEFAULT_SUBSET[cfg], 1)
+        r = one_config(cfg, sub or DEFAULT_SUBSET[cfg], 1, n_red)
         r["threads"] = int(os.environ.get("OMP_NUM_THREADS", threads))
         print(json.dumps(r), flush=True)
 
