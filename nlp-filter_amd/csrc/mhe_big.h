@@ -586,7 +586,8 @@ __global__ __launch_bounds__(256, 4) void k_big_assemble(BigArgs a) {
   const double* PhiE = (const double*)(a.cbuf + CL.PhiE);
   const int E = a.M > 0 ? *(const int*)(a.cbuf + CL.ne) : 0;
   const int E4 = (E + 3) & ~3;  // K steps of 4 epochs (av = bv = 0 past E)
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // wave-uniform work decomposition (SGPRs: the tile position, pair chunk and table reads are scalar)
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int NTc = a.NTc, P = a.P, NCH = a.nch;
   const int npos = NTc * (NTc + 1) / 2;
   const int u = blockIdx.x * 4 + wave;
@@ -613,27 +614,44 @@ __global__ __launch_bounds__(256, 4) void k_big_assemble(BigArgs a) {
 #pragma unroll
     for (int q = 0; q < BIG_PCH; ++q) goff[q] = q < np ? a.pa[q0 + q] * n + a.pb[q0 + q] : 0;
     // K steps of 4 epochs, software-pipelined: step e0 + 4's Phi_E and G_e loads are
-    // issued before step e0's MFMAs (clamped reads; padding epochs / rows zeroed)
-    double av, bv, gv[BIG_PCH];
-    auto issue = [&](int e0) {
-      const int e = e0 + (lane >> 4);
-      const int ec = e < E ? e : E - 1;
-      av = PhiE[(size_t)ec * P + (vr ? row : 0)];
-      bv = PhiE[(size_t)ec * P + (vc ? col : 0)];
-      if (!(e < E && vr)) av = 0.0;
-      if (!(e < E && vc)) bv = 0.0;
-      const double* gp = Ge + (size_t)ec * n * n;
+    // issued before step e0's MFMAs.  Raw buffer loads over exactly the E epochs: a lane
+    // past the last epoch (or on a padding row / column of the last tile) reads out of
+    // range and gets 0 from the hardware bounds check -- no clamps or selects, and the
+    // whole address is one 32-bit VGPR offset advanced by a constant per step.
+    const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc((void*)PhiE, (short)0, E * P * 8, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc((void*)Ge, (short)0, E * n * n * 8, 0x00020000);
+    constexpr int OOB = 0x40000000;
+    const int eg = lane >> 4;
+    int oa = vr ? (eg * P + row) * 8 : OOB, ob = vc ? (eg * P + col) * 8 : OOB, og = eg * n * n * 8;
+    int gs[BIG_PCH];  // byte offsets of G_e[ca][cb] in an epoch's block (wave-uniform)
 #pragma unroll
-      for (int q = 0; q < BIG_PCH; ++q) gv[q] = gp[goff[q]];
+    for (int q = 0; q < BIG_PCH; ++q) gs[q] = 8 * goff[q];
+    const int da = 4 * P * 8, dg = 4 * n * n * 8;
+    // two K steps in flight (loads for e0 + 4 and e0 + 8 issued before step e0's MFMAs)
+    double av1, bv1, gv1[BIG_PCH], av2, bv2, gv2[BIG_PCH];
+    auto issue = [&](double& av, double& bv, double (&gv)[BIG_PCH]) {
+      av = bload(rp, oa, 0);
+      bv = bload(rp, ob, 0);
+#pragma unroll
+      for (int q = 0; q < BIG_PCH; ++q) gv[q] = bload(rg, og + gs[q], 0);
+      oa += da;
+      ob += da;
+      og += dg;
     };
-    issue(0);
+    issue(av1, bv1, gv1);
+    issue(av2, bv2, gv2);
 #pragma unroll 1
     for (int e0 = 0; e0 < E4; e0 += 4) {
-      const double a0 = av, b0 = bv;
+      const double a0 = av1, b0 = bv1;
       double g0[BIG_PCH];
 #pragma unroll
-      for (int q = 0; q < BIG_PCH; ++q) g0[q] = gv[q];
-      if (e0 + 4 < E4) issue(e0 + 4);
+      for (int q = 0; q < BIG_PCH; ++q) {
+        g0[q] = gv1[q];
+        gv1[q] = gv2[q];
+      }
+      av1 = av2;
+      bv1 = bv2;
+      issue(av2, bv2, gv2);  // the last two read past E: zeros, unused
 #pragma unroll
       for (int q = 0; q < BIG_PCH; ++q)
         if (q < np) acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0 * g0[q], b0, acc[q], 0, 0, 0);
@@ -659,18 +677,28 @@ __global__ __launch_bounds__(256, 4) void k_big_assemble(BigArgs a) {
         if (lo[q] >= 0) acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(dv * (a2 * LAM[kc * n + lo[q]]), ev, acc[q], 0, 0, 0);
     }
   }
+  // element writes: raw buffer loads / stores with 32-bit offsets (one resource each over
+  // the constants, this trajectory's workspace and its H tiles), wave-uniform parts of
+  // every offset in SGPRs -- no 64-bit address arithmetic per element
+  const __amdgpu_buffer_rsrc_t rc = cbuf_rsrc(a.cbuf, CL.total);
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)ws, (short)0, (int)(WL.total * 8), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rh =
+      __builtin_amdgcn_make_buffer_rsrc((void*)H, (short)0, (int)((size_t)a.NT * (a.NT + 1) / 2 * 256 * 8), 0x00020000);
 #pragma unroll
   for (int q = 0; q < BIG_PCH; ++q) {
     if (q < np) {
       const int ca = a.pa[q0 + q], cb = a.pb[q0 + q];
       const double qab = a.huber ? 0.0 : a.alpha * a.alpha * Qw[ca * n + cb];
+      const double pw = a.has_prior ? Pw[ca * n + cb] : 0.0;
+      const int sE1 = (int)(WL.Es * 8) + (ca * n + cb) * 8, sE2 = (int)(WL.Es * 8) + (cb * n + ca) * 8;
+      const int sF = (int)(WL.FtE * 8) + (ca * n + cb) * 8;
       // tile (it, jt) of block (ca, cb) and, off the diagonal pair, its transpose into (jt, it)
 #pragma unroll
       for (int tp = 0; tp < 2; ++tp) {
         if (tp == 1 && (ca == cb || it == jt)) break;
         const int ti = tp ? jt : it, tj = tp ? it : jt;
         const int I = ca * NTc + ti, J = cb * NTc + tj;
-        double* tile = H + (size_t)big_tile_index(I, J, a.NT) * 256;
+        const int sT = big_tile_index(I, J, a.NT) * 256 * 8;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int cr = (lane >> 4) + 4 * r, cc = lane & 15;  // accumulator element (cr, cc) of tile (it, jt)
@@ -678,11 +706,11 @@ __global__ __launch_bounds__(256, 4) void k_big_assemble(BigArgs a) {
           const int j = 16 * ti + tr, l = 16 * tj + tc;
           double v;
           if (j < P && l < P) {
-            v = acc[q][r] + qab * DCD[(size_t)j * P + l] -
-                a.alpha * (D[(size_t)l * P + j] * ws[WL.Es + (l * n + ca) * n + cb] +
-                           D[(size_t)j * P + l] * ws[WL.Es + (j * n + cb) * n + ca]);
-            if (j == l) v += ws[WL.FtE + (j * n + ca) * n + cb];
-            if (a.has_prior && j == 0 && l == 0) v += Pw[ca * n + cb];
+            v = acc[q][r] + qab * bload(rc, (j * P + l) * 8, (int)CL.DCD) -
+                a.alpha * (bload(rc, (l * P + j) * 8, (int)CL.D) * bload(rw, l * n * n * 8, sE1) +
+                           bload(rc, (j * P + l) * 8, (int)CL.D) * bload(rw, j * n * n * 8, sE2));
+            if (j == l) v += bload(rw, j * n * n * 8, sF);
+            if (j == 0 && l == 0) v += pw;
           } else {
             v = (I == J && tr == tc) ? 1.0 : 0.0;
           }
@@ -691,7 +719,7 @@ __global__ __launch_bounds__(256, 4) void k_big_assemble(BigArgs a) {
             const int gr = 16 * I + tr, gc = 16 * J + tc;
             if ((ACT[gr] | ACT[gc]) && gr != gc) v = 0.0;
           }
-          tile[tr * 16 + tc] = v;
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(mhe_u2, v), rh, (tr * 16 + tc) * 8, sT, 0);
         }
       }
     }
