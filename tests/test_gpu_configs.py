@@ -159,3 +159,23 @@ def test_c5_eight_receivers_full_shape():
         s.ws_budget = None
     for x, y in zip(a, b):
         assert np.array_equal(x, y)
+
+
+def test_chunks_are_whole_cu_fulls():
+    """BatchSolver._chunk: a batch whose workspace does not fit is streamed in equal
+    chunks of whole CU-fulls when the budget allows more than one (C5: 2048 trajectories
+    at 0.52 GB each -> 8 x 256 on a 256-CU MI355X, not 5 x 410 with an idle tail round)."""
+    w = configs.make_c3(B=2, N=60)
+    s = solver.from_workload(w)
+    assert s.large_system
+    per = s.lib.mhe_workspace_bytes(s.dims, 1)
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    try:
+        s.ws_budget = per * (cus + cus // 2 + 10)
+        assert s._chunk(8 * cus) == cus
+        s.ws_budget = per * (cus // 2)
+        assert s._chunk(8 * cus) == cus // 2
+        s.ws_budget = None
+        assert s._chunk(3) == 3
+    finally:
+        s.ws_budget = None
