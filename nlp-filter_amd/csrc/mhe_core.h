@@ -2083,6 +2083,19 @@ int launch_big(const mhe_dims* dm, BigArgs& A, int batch, int max_iter, hipStrea
   if (hipFuncSetAttribute(wide ? (const void*)k_big_chol<8> : (const void*)k_big_chol<4>,
                           hipFuncAttributeMaxDynamicSharedMemorySize, smem) != hipSuccess)
     return MHE_ERR_HIP;
+  // split factorization (k_schol_*, several CUs per trajectory: 2.7x less HBM traffic but
+  // 9-13 % slower than k_big_chol); MHE_BIG_SPLIT=1 selects it (A/B runs)
+  const char* es = getenv("MHE_BIG_SPLIT");
+  const bool split = es ? atoi(es) != 0 : false;
+  const int smem_sd = big_schol_diag_lds() * (int)sizeof(double), smem_sr = big_schol_rows_lds() * (int)sizeof(double),
+            smem_st = big_schol_trail_lds() * (int)sizeof(double);
+  if (split && (hipFuncSetAttribute((const void*)k_schol_diag<BIG_SKB>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    smem_sd) != hipSuccess ||
+                hipFuncSetAttribute((const void*)k_schol_rows<BIG_SKB>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    smem_sr) != hipSuccess ||
+                hipFuncSetAttribute((const void*)k_schol_trail<BIG_SKB, BIG_SJB>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, smem_st) != hipSuccess))
+    return MHE_ERR_HIP;
   const int K = A.nz + A.nc;
   const int smem_b = (K * K + 2 * K) * (int)sizeof(double);
   if (K > 0 && hipFuncSetAttribute((const void*)k_big_border<DYN::n, MEAS::p>,
@@ -2101,10 +2114,24 @@ int launch_big(const mhe_dims* dm, BigArgs& A, int batch, int max_iter, hipStrea
   for (int it = 0; it < max_iter; ++it) {
     hipLaunchKernelGGL((k_big_resid<DYN, MEAS>), dim3(batch), dim3(BIG_NTHREADS), 0, st, A, 0);
     hipLaunchKernelGGL((k_big_assemble<DYN, MEAS>), dim3((npos * A.nch + 3) / 4, batch), dim3(256), 0, st, A);
-    if (wide)
+    if (split) {
+      for (int k0 = 0; k0 < A.NT; k0 += BIG_SKB) {
+        hipLaunchKernelGGL(k_schol_diag<BIG_SKB>, dim3(batch), dim3(BIG_NTHREADS), smem_sd, st, A, k0);
+        const int below = A.NT - min(k0 + BIG_SKB, A.NT);
+        if (below > 0) {
+          const int nsub = (below + 7) / 8;  // 8 rows per workgroup
+          const dim3 grid((unsigned)(8 * ((batch + 7) / 8) * nsub));
+          hipLaunchKernelGGL(k_schol_rows<BIG_SKB>, grid, dim3(BIG_NTHREADS), smem_sr, st, A, k0, nsub, batch);
+          hipLaunchKernelGGL((k_schol_trail<BIG_SKB, BIG_SJB>), grid, dim3(BIG_NTHREADS), smem_st, st, A, k0, nsub,
+                             batch);
+        }
+      }
+      hipLaunchKernelGGL(k_schol_back<BIG_SKB>, dim3(batch), dim3(BIG_NTHREADS), 0, st, A);
+    } else if (wide) {
       hipLaunchKernelGGL(k_big_chol<8>, dim3(batch), dim3(BIG_NTHREADS), smem, st, A);
-    else
+    } else {
       hipLaunchKernelGGL(k_big_chol<4>, dim3(batch), dim3(BIG_NTHREADS), smem, st, A);
+    }
     if (K > 0) hipLaunchKernelGGL((k_big_border<DYN::n, MEAS::p>), dim3(batch), dim3(BIG_NTHREADS), smem_b, st, A);
     if (bounded)
       hipLaunchKernelGGL((k_big_linesearch<DYN, MEAS>), dim3(batch), dim3(BIG_NTHREADS), smem_ls, st, A);
