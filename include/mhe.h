@@ -111,7 +111,7 @@ extern "C" {
  * the size queries) unless it equals this build's sizeof -- a binding that
  * declares an older or truncated struct is refused before any later field is
  * read.  (mhe/_lib.py sets it in the ctypes constructors.) */
-#define MHE_ABI_VERSION 3
+#define MHE_ABI_VERSION 4
 
 typedef struct mhe_dims {
   int32_t struct_size;  /* = sizeof(mhe_dims)                                */
@@ -338,6 +338,11 @@ int mhe_chol_solve(const mhe_dims* dims, const void* const_buf, int32_t batch,
 #define MHE_EKF_DYN_GNSS_POS_AND_BIAS 1          /* utils/gnss.py:79-90 (n=5, m=3, params dt) */
 #define MHE_EKF_MEAS_MULTI_PSEUDORANGE 1         /* utils/gnss.py:27-45 (q=3: sat ENU position) */
 #define MHE_EKF_MEAS_MULTI_PSEUDORANGE_AND_BIAS 2 /* utils/gnss.py:48-61 (last row: bias, zero Jacobian row) */
+/* the autonomous-car script's own EKF plug-ins (autonomous-car.py:18-77) */
+#define MHE_EKF_DYN_DISCRETE_VEHICLE 2           /* discrete_vehicle_dynamics :18-52 (n=9, m=2; params dt,
+                                                    car_params -> dyn_par = [C_AF, C_AR, M, D_F, D_R, I_Z]) */
+#define MHE_EKF_MEAS_VEHICLE_SENSORS 3           /* vehicle_sensors_model :54-77 (q=3: sat ENU position;
+                                                    rows of multi_pseudorange on x[0, 1, 8, 6, 7]) */
 
 typedef struct mhe_ekf_dims {
   int32_t struct_size; /* = sizeof(mhe_ekf_dims) */
@@ -357,6 +362,8 @@ typedef struct mhe_ekf_dims {
   int32_t in_batch_inner;   /* 1: U (steps, m, B), Z (steps, pmax, B), nz (steps, B), PAR
                                (steps, pmax, q, B) -- batch innermost (coalesced reads; the
                                *_bstride arguments are ignored); 0: the layouts below */
+  double dyn_par[8];        /* static dynamics parameters (MHE_EKF_DYN_DISCRETE_VEHICLE: the car
+                               constants; unused by gnss_pos_and_bias) */
 } mhe_ekf_dims;
 
 /*

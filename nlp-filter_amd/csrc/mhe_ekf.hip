@@ -27,9 +27,12 @@ constexpr int MAXP = 32;   // measurement rows per step (nz <= MAXP)
 // ---------------------------------------------------------------- plug-ins
 // gnss_pos_and_bias, utils/gnss.py:79-90: x+ = x + dt [u0, u1, u2, x4, 0],
 // G = I + dt e_3 e_4^T (the reference updates x in place; G does not depend on x).
+// gnz(r, c): structural non-zeros of G (compile-time; the predict skips the rest).
 struct EkfGnssPosAndBias {
   static constexpr int n = 5, m = 3;
-  __device__ static void step(const double* x, const double* u, double dt, double* xp, double* G) {
+  static constexpr bool gnz(int r, int c) { return r == c || (r == 3 && c == 4); }
+  __device__ static void step(const double* x, const double* u, double dt, const double* /*dp*/, double* xp,
+                              double* G) {
     xp[0] = x[0] + dt * u[0];
     xp[1] = x[1] + dt * u[1];
     xp[2] = x[2] + dt * u[2];
@@ -38,6 +41,74 @@ struct EkfGnssPosAndBias {
     for (int i = 0; i < n * n; ++i) G[i] = 0.0;
     for (int i = 0; i < n; ++i) G[i * n + i] = 1.0;
     G[3 * n + 4] = dt;
+  }
+};
+
+// discrete_vehicle_dynamics of autonomous-car.py:18-52 (a script-defined EKF plug-in):
+// x = [px, py, psi, vx, vy, r, b, bd, pz], u = [F_xr, delta]; explicit Euler on the
+// dynamic bicycle of utils/vehicle_sim.py:72-85 with the linear tyres of :58-66
+// (slip angles (vy -+ D r)/vx, no epsilon), plus b+ = b + dt bd.
+// dp = car_params as [C_AF, C_AR, M, D_F, D_R, I_Z].  Bug-compatible with the
+// reference: x is updated IN PLACE before the Jacobian is formed (autonomous-car.py:23),
+// so every entry of G below is evaluated at the PREDICTED state x+, and G holds exactly
+// the entries the reference writes.
+struct EkfDiscreteVehicle {
+  static constexpr int n = 9, m = 2;
+  static constexpr bool gnz(int r, int c) {
+    return r == c || ((r == 0 || r == 1) && c >= 2 && c <= 4) || (r == 2 && c == 5) ||
+           (r >= 3 && r <= 5 && c >= 3 && c <= 5) || (r == 6 && c == 7);
+  }
+  __device__ static void step(const double* x, const double* u, double dt, const double* dp, double* xp,
+                              double* G) {
+    const double C_AF = dp[0], C_AR = dp[1], Mv = dp[2], D_F = dp[3], D_R = dp[4], I_Z = dp[5];
+    {  // xd at x (utils/vehicle_sim.py:72-85 with linear_tire_model)
+      const double a_r = (x[4] - D_R * x[5]) / x[3];
+      const double a_f = (x[4] + D_F * x[5]) / x[3] - u[1];
+      const double F_yr = -C_AR * a_r, F_yf = -C_AF * a_f;
+      double sp, cp, su, cu;
+      sincos(x[2], &sp, &cp);
+      sincos(u[1], &su, &cu);
+      xp[0] = x[0] + dt * (x[3] * cp - x[4] * sp);
+      xp[1] = x[1] + dt * (x[3] * sp + x[4] * cp);
+      xp[2] = x[2] + dt * x[5];
+      xp[3] = x[3] + dt * ((-F_yf * su + u[0]) / Mv + x[5] * x[4]);
+      xp[4] = x[4] + dt * ((F_yf * cu + F_yr) / Mv - x[5] * x[3]);
+      xp[5] = x[5] + dt * ((D_F * F_yf * cu - D_R * F_yr) / I_Z);
+      xp[6] = x[6] + dt * x[7];
+      xp[7] = x[7] + dt * 0.0;
+      xp[8] = x[8] + dt * 0.0;
+    }
+    // Jacobian at x+ (autonomous-car.py:27-51)
+    const double* y = xp;
+    const double ivx = 1.0 / (y[3] * y[3]);
+    const double dfyf_dvx = C_AF * (y[4] + D_F * y[5]) * ivx;
+    const double dfyf_dvy = -C_AF / y[3];
+    const double dfyf_dr = -C_AF * D_F / y[3];
+    const double dfyr_dvx = C_AR * (y[4] - D_R * y[5]) * ivx;
+    const double dfyr_dvy = -C_AR / y[3];
+    const double dfyr_dr = C_AR * D_R / y[3];
+    double sp, cp, su, cu;
+    sincos(y[2], &sp, &cp);
+    sincos(u[1], &su, &cu);
+    for (int i = 0; i < n * n; ++i) G[i] = 0.0;
+    for (int i = 0; i < n; ++i) G[i * n + i] = 1.0;
+    G[0 * n + 2] += dt * (-y[3] * sp - y[4] * cp);
+    G[0 * n + 3] += dt * cp;
+    G[0 * n + 4] += -dt * sp;
+    G[1 * n + 2] += dt * (y[3] * cp - y[4] * sp);
+    G[1 * n + 3] += dt * sp;
+    G[1 * n + 4] += dt * cp;
+    G[2 * n + 5] += dt;
+    G[3 * n + 3] += -(dt / Mv) * (su * dfyf_dvx);
+    G[3 * n + 4] += dt * (y[5] - (su * dfyf_dvy) / Mv);
+    G[3 * n + 5] += dt * (y[4] - (su * dfyf_dr) / Mv);
+    G[4 * n + 3] += dt * ((cu * dfyf_dvx + dfyr_dvx) / Mv - y[5]);
+    G[4 * n + 4] += (dt / Mv) * (cu * dfyf_dvy + dfyr_dvy);
+    G[4 * n + 5] += dt * ((cu * dfyf_dr + dfyr_dr) / Mv - y[3]);
+    G[5 * n + 3] += (dt / I_Z) * (D_F * cu * dfyf_dvx - D_R * dfyr_dvx);
+    G[5 * n + 4] += (dt / I_Z) * (D_F * cu * dfyf_dvy - D_R * dfyr_dvy);
+    G[5 * n + 5] += (dt / I_Z) * (D_F * cu * dfyf_dr - D_R * dfyr_dr);
+    G[6 * n + 7] += dt;
   }
 };
 
@@ -67,9 +138,29 @@ struct EkfMultiPseudorange {
   }
 };
 
+// vehicle_sensors_model of autonomous-car.py:54-77: multi_pseudorange on
+// x_meas = [px, py, pz, b, bd] = x[0, 1, 8, 6, 7]; row i: h = |p - s_i| + b and the
+// 5-column Jacobian scattered back to the 9-state (columns 0, 1, 8, 6, 7).
+struct EkfVehicleSensors {
+  static constexpr int q = 3;
+  template <int n>
+  __device__ static void row(const double* x, const double* par, int /*i*/, int /*nz*/, double& h, double* H) {
+    const double l0 = par[0] - x[0], l1 = par[1] - x[1], l2 = par[2] - x[8];
+    const double r = sqrt(l0 * l0 + l1 * l1 + l2 * l2);
+    h = sqrt((x[0] - par[0]) * (x[0] - par[0]) + (x[1] - par[1]) * (x[1] - par[1]) +
+             (x[8] - par[2]) * (x[8] - par[2])) + x[6];
+    for (int c = 0; c < n; ++c) H[c] = 0.0;
+    H[0] = -l0 / r;
+    H[1] = -l1 / r;
+    H[8] = -l2 / r;
+    H[6] = 1.0;
+  }
+};
+
 struct EkfArgs {
   int batch, steps, nmeas_rows_max;
   double dt;
+  double dp[8];  // static dynamics parameters (mhe_ekf_dims.dyn_par)
   double* mu;
   double* S;
   const double* U;
@@ -140,7 +231,7 @@ __global__ __launch_bounds__(NWF * 64) void k_ekf(EkfArgs a) {
       double x[n], u[m > 0 ? m : 1], xp[n], Gl[n * n];
       for (int c = 0; c < n; ++c) x[c] = mu[c];
       for (int c = 0; c < m; ++c) u[c] = a.U[(long long)b * a.u_bstride + ((long long)k * m + c) * a.es];
-      DYN::step(x, u, a.dt, xp, Gl);
+      DYN::step(x, u, a.dt, a.dp, xp, Gl);
       for (int c = 0; c < n; ++c) MP[c] = xp[c];
       for (int c = 0; c < n * n; ++c) G[c] = Gl[c];
     }
@@ -264,42 +355,64 @@ __global__ __launch_bounds__(NWF * 64) void k_ekf(EkfArgs a) {
 // The whole filter lives in one lane's registers (mu, mu-, S: 35 doubles), so a
 // wave runs 64 filters with no broadcasts, barriers or LDS: O(p n^2) work per
 // step instead of the sweep's O(p^3), and no lane idles on the row loop.
+// S storage in one lane: full n x n for small n; for larger n (the 9-state vehicle)
+// the upper triangle only (45 instead of 81 doubles, so S and S- fit the registers).
+// The symmetric form reads S[r][c] = S[c][r] = stored (min, max) entry.
+template <int n>
+struct LaneS {
+  static constexpr bool sym = n > 6;
+  static constexpr int size = sym ? n * (n + 1) / 2 : n * n;
+  static constexpr int at(int r, int c) {
+    return sym ? (r <= c ? r * n - r * (r - 1) / 2 + (c - r) : c * n - c * (c - 1) / 2 + (r - c)) : r * n + c;
+  }
+};
+
 template <class DYN, class MEAS>
 __global__ __launch_bounds__(256) void k_ekf_lane(EkfArgs a) {
   constexpr int n = DYN::n, m = DYN::m, q = MEAS::q;
+  using LS = LaneS<n>;
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= a.batch) return;  // no barriers below
-  double mu[n], S[n * n];
+  double mu[n], S[LS::size];
 #pragma unroll
   for (int c = 0; c < n; ++c) mu[c] = a.mu[(size_t)b * n + c];
 #pragma unroll
-  for (int c = 0; c < n * n; ++c) S[c] = a.S[(size_t)b * n * n + c];
+  for (int r = 0; r < n; ++r)
+#pragma unroll
+    for (int c = 0; c < n; ++c)
+      if (!LS::sym || c >= r) S[LS::at(r, c)] = a.S[(size_t)b * n * n + r * n + c];
   int status = 0;
   for (int k = 0; k < a.steps; ++k) {
-    // ---- predict: mu- = f(mu, u), S- = G S G^T + Q   (utils/ekf.py:40-45)
+    // ---- predict: mu- = f(mu, u), S- = G S G^T + Q   (utils/ekf.py:40-45); only the
+    // structural non-zeros of G (DYN::gnz, compile time) enter the products
     double u[m > 0 ? m : 1], mp[n], G[n * n];
 #pragma unroll
     for (int c = 0; c < m; ++c) u[c] = a.U[(long long)b * a.u_bstride + ((long long)k * m + c) * a.es];
-    DYN::step(mu, u, a.dt, mp, G);
-    double GS[n * n];
+    DYN::step(mu, u, a.dt, a.dp, mp, G);
+    double SN[LS::size];
 #pragma unroll
-    for (int r = 0; r < n; ++r)
+    for (int c = 0; c < n; ++c) {
+      double v[n];  // (S G^T)[:, c]
 #pragma unroll
-      for (int c = 0; c < n; ++c) {
+      for (int l = 0; l < n; ++l) {
         double acc = 0.0;
 #pragma unroll
-        for (int l = 0; l < n; ++l) acc += G[r * n + l] * S[l * n + c];
-        GS[r * n + c] = acc;
+        for (int kk = 0; kk < n; ++kk)
+          if (DYN::gnz(c, kk)) acc += S[LS::at(l, kk)] * G[c * n + kk];
+        v[l] = acc;
       }
 #pragma unroll
-    for (int r = 0; r < n; ++r)
-#pragma unroll
-      for (int c = 0; c < n; ++c) {
+      for (int r = 0; r < n; ++r) {
+        if (LS::sym && r > c) continue;
         double acc = 0.0;
 #pragma unroll
-        for (int l = 0; l < n; ++l) acc += GS[r * n + l] * G[c * n + l];
-        S[r * n + c] = acc + a.Q[r * n + c];
+        for (int l = 0; l < n; ++l)
+          if (DYN::gnz(r, l)) acc += G[r * n + l] * v[l];
+        SN[LS::at(r, c)] = acc + a.Q[r * n + c];
       }
+    }
+#pragma unroll
+    for (int i = 0; i < LS::size; ++i) S[i] = SN[i];
 #pragma unroll
     for (int c = 0; c < n; ++c) mu[c] = mp[c];
     // ---- correct: sequential scalar updates at the linearisation point mu-
@@ -337,7 +450,7 @@ __global__ __launch_bounds__(256) void k_ekf_lane(EkfArgs a) {
         for (int r = 0; r < n; ++r) {
           double acc = 0.0;
 #pragma unroll
-          for (int c = 0; c < n; ++c) acc += S[r * n + c] * H[c];
+          for (int c = 0; c < n; ++c) acc += S[LS::at(r, c)] * H[c];
           v[r] = acc;
         }
         double sv = rr[u];
@@ -352,7 +465,8 @@ __global__ __launch_bounds__(256) void k_ekf_lane(EkfArgs a) {
         for (int r = 0; r < n; ++r) {
           const double vr = v[r] * inv;
 #pragma unroll
-          for (int c = 0; c < n; ++c) S[r * n + c] -= vr * v[c];
+          for (int c = 0; c < n; ++c)
+            if (!LS::sym || c >= r) S[LS::at(r, c)] -= vr * v[c];
         }
       }
     }
@@ -364,13 +478,17 @@ __global__ __launch_bounds__(256) void k_ekf_lane(EkfArgs a) {
     }
     if (a.S_hist) {
 #pragma unroll
-      for (int c = 0; c < n * n; ++c) a.S_hist[hist_at(a, b, k, c, n * n)] = S[c];
+      for (int r = 0; r < n; ++r)
+#pragma unroll
+        for (int c = 0; c < n; ++c) a.S_hist[hist_at(a, b, k, r * n + c, n * n)] = S[LS::at(r, c)];
     }
   }
 #pragma unroll
   for (int c = 0; c < n; ++c) a.mu[(size_t)b * n + c] = mu[c];
 #pragma unroll
-  for (int c = 0; c < n * n; ++c) a.S[(size_t)b * n * n + c] = S[c];
+  for (int r = 0; r < n; ++r)
+#pragma unroll
+    for (int c = 0; c < n; ++c) a.S[(size_t)b * n * n + r * n + c] = S[LS::at(r, c)];
   if (a.status) a.status[b] = status;
 }
 
@@ -410,14 +528,23 @@ extern "C" int mhe_ekf_run(const mhe_ekf_dims* dims, int32_t batch, int32_t step
     a.u_bstride = a.z_bstride = a.nz_bstride = a.par_bstride = 1;
   }
   hipStream_t st = (hipStream_t)stream;
-  if (dims->dyn_model != MHE_EKF_DYN_GNSS_POS_AND_BIAS || dims->n != 5 || dims->m != 3) return MHE_ERR_MODEL;
+  for (int i = 0; i < 8; ++i) a.dp[i] = dims->dyn_par[i];
   if (dims->q != 3) return MHE_ERR_DIMS;
   if (!PAR) return MHE_ERR_NULL;
-  switch (dims->meas_model) {
-    case MHE_EKF_MEAS_MULTI_PSEUDORANGE:
-      return launch<EkfGnssPosAndBias, EkfMultiPseudorange<false>>(a, st, dims->r_diag != 0);
-    case MHE_EKF_MEAS_MULTI_PSEUDORANGE_AND_BIAS:
-      return launch<EkfGnssPosAndBias, EkfMultiPseudorange<true>>(a, st, dims->r_diag != 0);
+  const bool rd = dims->r_diag != 0;
+  if (dims->dyn_model == MHE_EKF_DYN_GNSS_POS_AND_BIAS) {
+    if (dims->n != 5 || dims->m != 3) return MHE_ERR_MODEL;
+    switch (dims->meas_model) {
+      case MHE_EKF_MEAS_MULTI_PSEUDORANGE:
+        return launch<EkfGnssPosAndBias, EkfMultiPseudorange<false>>(a, st, rd);
+      case MHE_EKF_MEAS_MULTI_PSEUDORANGE_AND_BIAS:
+        return launch<EkfGnssPosAndBias, EkfMultiPseudorange<true>>(a, st, rd);
+    }
+  } else if (dims->dyn_model == MHE_EKF_DYN_DISCRETE_VEHICLE) {
+    if (dims->n != 9 || dims->m != 2) return MHE_ERR_MODEL;
+    if (!(dims->dyn_par[2] != 0.0 && dims->dyn_par[5] != 0.0)) return MHE_ERR_DIMS;  // M, I_Z unset
+    if (dims->meas_model == MHE_EKF_MEAS_VEHICLE_SENSORS)
+      return launch<EkfDiscreteVehicle, EkfVehicleSensors>(a, st, rd);
   }
   return MHE_ERR_MODEL;
 }

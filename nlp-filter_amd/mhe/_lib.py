@@ -43,7 +43,7 @@ class MheDims(_Sized):
 class MheEkfDims(_Sized):
     _fields_ = [("struct_size", c_i32), ("n", c_i32), ("m", c_i32), ("pmax", c_i32), ("q", c_i32),
                 ("dyn_model", c_i32), ("meas_model", c_i32), ("dt", c_dbl), ("r_diag", c_i32),
-                ("hist_batch_inner", c_i32), ("in_batch_inner", c_i32)]
+                ("hist_batch_inner", c_i32), ("in_batch_inner", c_i32), ("dyn_par", c_dbl * 8)]
 
 
 class MheLsDims(_Sized):

@@ -6,8 +6,12 @@ and semantics (utils/ekf.py:11-38): ``mu`` / ``S`` are NumPy arrays replaced by
 each update; ``z=None`` predicts only.  Each update is one launch of
 ``mhe_ekf_run`` (csrc/mhe_ekf.hip); ``run_batch`` runs many independent filter
 instances over many steps in a single launch (the GPU-shaped entry point).
-Plug-ins are resolved by name (``utils.gnss.EKF_DYN`` / ``EKF_MEAS``); an
-unregistered plug-in raises ``UnsupportedPlugin`` -- there is no CPU path.
+Plug-ins are resolved by name (``utils.gnss.EKF_DYN`` / ``EKF_MEAS``: the
+utils/gnss.py models and autonomous-car.py's own ``discrete_vehicle_dynamics`` /
+``vehicle_sensors_model``); a user's callable is then evaluated at seeded points
+against the registered twin (``utils.gnss``, ``utils.vehicle``) and refused on any
+difference.  An unregistered or mismatching plug-in raises ``UnsupportedPlugin`` --
+there is no CPU path.
 
 Numerics: the reference forms inv(P) (utils/ekf.py:55); the kernel uses a
 Cholesky sweep of P, so results agree to floating-point rounding (tests state
@@ -21,6 +25,7 @@ from mhe import _lib
 from mhe.registry import UnsupportedPlugin
 
 from . import gnss as _gnss
+from . import vehicle as _vehicle
 
 MAXP = 32
 
@@ -35,7 +40,87 @@ def models(dyn_func, meas_func):
         raise UnsupportedPlugin(f"EKF dynamics plug-in {dn!r} has no HIP functor; registered: {sorted(_gnss.EKF_DYN)}")
     if mn not in _gnss.EKF_MEAS:
         raise UnsupportedPlugin(f"EKF measurement plug-in {mn!r} has no HIP functor; registered: {sorted(_gnss.EKF_MEAS)}")
+    if (dn, mn) not in _gnss.EKF_PAIRS:
+        raise UnsupportedPlugin(f"EKF pair ({dn!r}, {mn!r}) is not compiled into libmhe.so; "
+                                f"available: {sorted(_gnss.EKF_PAIRS)}")
     return _gnss.EKF_DYN[dn], _gnss.EKF_MEAS[mn]
+
+
+def dyn_par(dyn_func, params):
+    """mhe_ekf_dims.dyn_par for a dynamics plug-in and its dyn_func_params."""
+    out = np.zeros(8)
+    if _name(dyn_func) == "discrete_vehicle_dynamics":
+        C = (params or {}).get("car_params")
+        if C is None:
+            raise UnsupportedPlugin("discrete_vehicle_dynamics needs dyn_func_params['car_params'] "
+                                    "(autonomous-car.py:160)")
+        out[:6] = [float(C[k]) for k in _vehicle.CAR_KEYS]
+    return out
+
+
+# ---------------------------------------------------------------- identity checks
+_VERIFIED = {}
+
+
+def _twin(name):
+    for mod in (_gnss, _vehicle):
+        if hasattr(mod, name):
+            return getattr(mod, name)
+    raise UnsupportedPlugin(f"EKF plug-in {name!r} has no registered twin to verify against")
+
+
+def _close(a, b, rtol=1e-12):
+    a, b = np.asarray(a, dtype=np.float64), np.asarray(b, dtype=np.float64)
+    return a.shape == b.shape and bool(np.all(np.abs(a - b) <= rtol * (1.0 + np.abs(b))))
+
+
+def _params_key(p):
+    if not p:
+        return ()
+    return tuple(sorted((k, _params_key(v) if isinstance(v, dict) else float(v)) for k, v in p.items()
+                        if isinstance(v, (dict, int, float, np.floating, np.integer))))
+
+
+def verify(dyn_func, meas_func, dyn_params):
+    """Refuse (UnsupportedPlugin) user callables whose values or Jacobians differ from
+    the registered twins at 4 seeded points: a same-named plug-in with other math or
+    other constants must not silently get the built-in device functor.  Strings and this
+    package's own functions pass without evaluation; results are cached per callable
+    and parameter values."""
+    (_, n, m), (_, _, q) = models(dyn_func, meas_func)
+    for fn, kind in ((dyn_func, "dyn"), (meas_func, "meas")):
+        if isinstance(fn, str):
+            continue
+        twin = _twin(_name(fn))
+        if fn is twin:
+            continue
+        key = (id(fn), kind, _params_key(dyn_params) if kind == "dyn" else ())
+        if _VERIFIED.get(key) is fn:
+            continue
+        rng = np.random.default_rng(20262)
+        for _ in range(4):
+            x = rng.normal(size=n) * 3.0
+            if n == 9:
+                x[3] = 5.0 + abs(x[3])   # forward speed away from the tyre model's pole at vx = 0
+            try:
+                if kind == "dyn":
+                    u = rng.normal(size=m)
+                    got = fn(x.copy(), u, params=dyn_params, jac=True)
+                    ref = twin(x.copy(), u, params=dyn_params, jac=True)
+                else:
+                    p = {"sat_pos": rng.normal(size=(4, 3)) * 2.0e4}
+                    got = fn(x.copy(), params=p, jac=True)
+                    ref = twin(x.copy(), params=p, jac=True)
+            except UnsupportedPlugin:
+                raise
+            except Exception as e:
+                raise UnsupportedPlugin(f"EKF plug-in {_name(fn)!r} could not be evaluated to verify it matches "
+                                        f"the device functor: {type(e).__name__}: {e}") from e
+            if not (_close(got[0], ref[0]) and _close(got[1], ref[1])):
+                raise UnsupportedPlugin(f"EKF plug-in {_name(fn)!r} is not the registered {_name(fn)}: its values "
+                                        "or Jacobian differ from the device functor's (same name, different math "
+                                        "or constants)")
+        _VERIFIED[key] = fn
 
 
 def _ptr(t):
@@ -43,12 +128,14 @@ def _ptr(t):
 
 
 def run_batch(dyn_func, meas_func, mu0, S0, U, Z, nz, Q, R, dt, sat_pos, device=None, stream=None,
-              keep_history=True, method="auto", inputs="batch_outer"):
+              keep_history=True, method="auto", inputs="batch_outer", dyn_params=None):
     """Run B independent filters for T steps in one launch.
 
     mu0 (B,n), S0 (B,n,n), U (B,T,m), Z (B,T,pmax), nz (B,T) valid rows per step
     (0 = predict only), Q (n,n), R (T,pmax,pmax) or (B,T,pmax,pmax), sat_pos
-    (B,T,pmax,3); dt = dyn_func_params["dt"].  Inputs may be NumPy or torch.
+    (B,T,pmax,3); dt = dyn_func_params["dt"]; dyn_params = the whole dyn_func_params
+    (needed for discrete_vehicle_dynamics: "car_params"; its "dt", when given, wins
+    over dt).  Inputs may be NumPy or torch.
     Returns (mu_hist (B,T,n), S_hist (B,T,n,n), mu (B,n), S (B,n,n), status (B))
     as torch tensors on the device.
 
@@ -66,14 +153,18 @@ def run_batch(dyn_func, meas_func, mu0, S0, U, Z, nz, Q, R, dt, sat_pos, device=
     from mhe.streams import launch_stream
 
     (did, n, m), (mid, _, q) = models(dyn_func, meas_func)
+    if dyn_params is not None and "dt" in dyn_params:
+        dt = dyn_params["dt"]
+    verify(dyn_func, meas_func, dict(dyn_params or {}, dt=dt))
+    dp = dyn_par(dyn_func, dyn_params)
     dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
     with launch_stream(stream, dev) as (s, cur):
         return _run_batch(did, n, m, mid, q, dev, s, cur, mu0, S0, U, Z, nz, Q, R, dt, sat_pos, keep_history,
-                          method, inputs)
+                          method, inputs, dp)
 
 
 def _run_batch(did, n, m, mid, q, dev, s, cur, mu0, S0, U, Z, nz, Q, R, dt, sat_pos, keep_history, method,
-               inputs):
+               inputs, dp):
     """run_batch on torch stream s (staging and allocation ordered on s)."""
     import torch
 
@@ -124,6 +215,8 @@ def _run_batch(did, n, m, mid, q, dev, s, cur, mu0, S0, U, Z, nz, Q, R, dt, sat_
         raise ValueError(f"unknown method {method!r}")
     dims = _lib.MheEkfDims(n=n, m=m, pmax=pmax, q=q, dyn_model=did, meas_model=mid, dt=float(dt),
                            r_diag=int(r_diag), hist_batch_inner=1, in_batch_inner=int(bi))
+    for i in range(8):
+        dims.dyn_par[i] = float(dp[i])
     lib = _lib.load()
     rc = lib.mhe_ekf_run(ctypes.byref(dims), B, T, _ptr(mu), _ptr(S), _ptr(Ut), T * m, _ptr(Zt), T * pmax,
                          _ptr(nzt), T, _ptr(Pt), T * pmax * q, _ptr(Qt), _ptr(Rt), r_b, r_s, _ptr(mh_st),
@@ -169,7 +262,8 @@ class EKF(object):
             P[0, 0, :sp.shape[0]] = sp
             Rm = np.asarray(R, dtype=np.float64).reshape(1, pmax, pmax)
         _, _, mu, S, st = run_batch(self.dynamics, meas, mu0, S0, u_, Z, np.full((1, 1), nz, np.int32),
-                                    np.asarray(Q, dtype=np.float64), Rm, dt, P, keep_history=False)
+                                    np.asarray(Q, dtype=np.float64), Rm, dt, P, keep_history=False,
+                                    dyn_params=dyn_func_params)
         if int(st[0].item()) != 0:
             raise np.linalg.LinAlgError("innovation covariance is not positive definite")
         self.mu = mu[0].cpu().numpy()

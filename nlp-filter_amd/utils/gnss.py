@@ -53,6 +53,12 @@ def gnss_pos_and_bias(x, u, params=None, jac=False):
     return x
 
 
-# name -> (model id, n, m) / (model id, extra rows, q); include/mhe.h MHE_EKF_*
-EKF_DYN = {"gnss_pos_and_bias": (1, 5, 3)}
-EKF_MEAS = {"multi_pseudorange": (1, 0, 3), "multi_pseudorange_and_bias": (2, 1, 3)}
+# name -> (model id, n, m) / (model id, extra rows, q); include/mhe.h MHE_EKF_*.
+# discrete_vehicle_dynamics / vehicle_sensors_model are autonomous-car.py's own
+# plug-ins (twins in utils/vehicle.py).
+EKF_DYN = {"gnss_pos_and_bias": (1, 5, 3), "discrete_vehicle_dynamics": (2, 9, 2)}
+EKF_MEAS = {"multi_pseudorange": (1, 0, 3), "multi_pseudorange_and_bias": (2, 1, 3),
+            "vehicle_sensors_model": (3, 0, 3)}
+# which measurement plug-ins each dynamics functor is compiled with (csrc/mhe_ekf.hip)
+EKF_PAIRS = {("gnss_pos_and_bias", "multi_pseudorange"), ("gnss_pos_and_bias", "multi_pseudorange_and_bias"),
+             ("discrete_vehicle_dynamics", "vehicle_sensors_model")}

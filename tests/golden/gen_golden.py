@@ -13,6 +13,9 @@ What it does
     the reference's own ``__init__`` runs unmodified;
   * imports ``utils/ekf.py`` and ``utils/gnss.py`` (flat imports, as the survey
     documents) and runs the reference EKF on the gnss_stationary log;
+  * runs the reference EKF with autonomous-car.py's own plug-ins (their two function
+    definitions taken from the script's syntax tree; the script itself loads pickles
+    and is not imported) on seeded data of the script's shape;
   * stores ONLY numbers (inputs and outputs) -- no reference source or bytecode
     is written into this repository.
 
@@ -439,10 +442,86 @@ def gen_c3_geometry(ref):
                         t=np.asarray(list(data["t"]), dtype=np.float64)[:E])
 
 
+def load_autocar_plugins(ref):
+    """autonomous-car.py defines its EKF plug-ins (:18-77) at module level next to code
+    that loads its pickled inputs, so the script is not imported: the two function
+    definitions are taken from its syntax tree and executed in a namespace holding
+    the modules they use (numpy, the reference's utils/vehicle_sim.py and utils/gnss.py)."""
+    import ast
+    path = f"{REF}/autonomous-car.py"
+    tree = ast.parse(open(path).read(), filename=path)
+    keep = [n for n in tree.body if isinstance(n, ast.FunctionDef)
+            and n.name in ("discrete_vehicle_dynamics", "vehicle_sensors_model")]
+    ns = {"np": np, "vehicle_sim": ref.vehicle_sim, "gnss": ref.gnss}
+    exec(compile(ast.Module(body=keep, type_ignores=[]), path, "exec"), ns)
+    return ns["discrete_vehicle_dynamics"], ns["vehicle_sensors_model"]
+
+
+def gen_autocar_ekf(ref):
+    """The reference EKF with autonomous-car.py's own plug-ins (:18-77), driven as the
+    script's loop (:120-178: dt = 0.01, a correction at every 10th step, R = r_pr I,
+    Q_EKF = 1e-3 Q_NLP, P = I) on seeded data of the script's shape (its sim pickles are
+    not readable here): a linear-tyre bicycle trajectory from the reference's own
+    vehicle_dynamics, 8-11 satellites per epoch in ENU, clock b0 + alpha t."""
+    fdyn, fmeas = load_autocar_plugins(ref)
+    car = ref.vehicle_sim.get_parameters()
+    rng = np.random.default_rng(4242)
+    dt, steps, every = 0.01, 300, 10
+    t = dt * np.arange(steps)
+    U = np.stack([1500.0 + 800.0 * np.sin(0.35 * t), 0.04 * np.sin(0.5 * t + 0.3)], axis=1)
+    x = np.array([0.0, 0.0, 0.3, 8.0, 0.0, 0.0])
+    xs = []
+    for k in range(steps):
+        xs.append(x.copy())
+        x = x + dt * ref.vehicle_sim.vehicle_dynamics(x, U[k], {"tire_model_func": ref.vehicle_sim.linear_tire_model})
+    xs = np.array(xs)
+    NS, r_pr, alpha, b0 = 11, 10.0, 200.0, 0.0
+    dirs = rng.normal(size=(NS, 3))
+    dirs[:, 2] = np.abs(dirs[:, 2]) + 0.3
+    sats = 2.0e7 * dirs / np.linalg.norm(dirs, axis=1, keepdims=True)
+    Z = np.zeros((steps, NS)); SP = np.zeros((steps, NS, 3)); nz = np.zeros(steps, np.int32)
+    for k in range(0, steps, every):
+        ns = int(rng.integers(8, NS + 1))
+        p = np.array([xs[k, 0], xs[k, 1], 0.0])
+        SP[k, :ns] = sats[:ns]
+        Z[k, :ns] = np.linalg.norm(p - sats[:ns], axis=1) + b0 + alpha * t[k] + np.sqrt(r_pr) * rng.normal(size=ns)
+        nz[k] = ns
+    Q_NLP = np.diag([0.01, 0.01, 0.01, 100, 500, 500, .001, .001, .001])
+    Q = .001 * Q_NLP
+    mu0 = np.hstack((xs[0], np.array([b0, alpha, 0.0])))
+    S0 = np.diag(np.ones(9))
+    filt = ref.ekf.EKF(fdyn, fmeas, mu0.copy(), S0.copy())
+    mus, Ss = [], []
+    for k in range(steps):
+        ns = int(nz[k])
+        z = Z[k, :ns] if ns else None
+        R = np.diag(r_pr * np.ones(ns)) if ns else None
+        filt.update(U[k], z, Q, R, dyn_func_params={"dt": dt, "car_params": car},
+                    meas_func_params={"sat_pos": SP[k, :ns] if ns else None})
+        mus.append(np.array(filt.mu, dtype=np.float64).copy()); Ss.append(np.array(filt.S, dtype=np.float64).copy())
+    # plug-in values / Jacobians at seeded points (the reference's own jac=True outputs)
+    px = rng.normal(size=(32, 9)) * 3.0
+    px[:, 3] = 4.0 + np.abs(px[:, 3]) * 5.0
+    pu = rng.normal(size=(32, 2)) * np.array([1500.0, 0.1])
+    pf, pF, py, pH, ps = [], [], [], [], []
+    for xx, uu in zip(px, pu):
+        f0, J = fdyn(xx.copy(), uu, params={"dt": dt, "car_params": car}, jac=True)
+        pf.append(f0); pF.append(J)
+        s = rng.normal(size=(5, 3)) * 2.0e4
+        y0, H = fmeas(xx.copy(), params={"sat_pos": s}, jac=True)
+        py.append(y0); pH.append(H); ps.append(s)
+    np.savez_compressed(os.path.join(OUT, "ekf_autocar.npz"), mu0=mu0, S0=S0, Q=Q, r_pr=np.array(r_pr), dt=np.array(dt),
+                        car=np.array([car[k] for k in ("C_AF", "C_AR", "M", "D_F", "D_R", "I_Z")]),
+                        U=U, Z=Z, sat_pos=SP, nz=nz, mu=np.stack(mus), S=np.stack(Ss)[::5], S_every=np.array(5),
+                        plug_x=px, plug_u=pu, plug_f=np.stack(pf), plug_F=np.stack(pF), plug_sat=np.stack(ps),
+                        plug_y=np.stack(py), plug_H=np.stack(pH))
+
+
 def main(which=None):
     ref = load_reference()
     gens = {"collocation": gen_collocation, "plugins": gen_plugins, "ekf": gen_ekf, "gnss_io": gen_gnss_io,
-            "least_squares": gen_least_squares, "c3_geometry": gen_c3_geometry}
+            "least_squares": gen_least_squares, "c3_geometry": gen_c3_geometry,
+            "autocar_ekf": gen_autocar_ekf}
     for name, fn in gens.items():
         if not which or name in which:
             fn(ref)
