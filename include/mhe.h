@@ -147,6 +147,10 @@ typedef struct mhe_dims {
                            solve checks that stamp on the device.                 */
   double dyn_par[8];    /* static dynamics parameters (model-defined, e.g.
                            MHE_DYN_VEHICLE_GNSS); 0 for the parameter-free models   */
+  const double* eq_rhs; /* HOST pointer, n_eq constants r_i of the rows
+                           v[a] - v[b] = r_i, or NULL (all 0: addEqConstraint rows).
+                           Non-zero r: the rows an active set imposes (bounds and
+                           inequality constraints held at equality by the host) */
 } mhe_dims;
 
 /* Dynamics cost (addDynamicsCost, nlp/nlp.py:242-245): */
@@ -291,6 +295,9 @@ typedef struct mhe_solve_args {
   double tol;
   void* workspace;         /* large-system path: >= mhe_workspace_bytes(dims, batch) */
   size_t workspace_bytes;
+  double* lambda_out;      /* optional (B, n_eq): multipliers of the constraint rows from the
+                              last bordered step, L = J + lambda^T (C v - r) (their signs
+                              drive the host's active set), or NULL */
 } mhe_solve_args;
 
 int mhe_solve(const mhe_dims* dims, const void* const_buf, const mhe_solve_args* args, void* stream);

@@ -33,7 +33,7 @@ constexpr int BIG_RUNNING = -1;
 __host__ __device__ inline int big_pp(int P) { return 16 * ((P + 15) / 16); }
 
 struct BigConst {  // byte offsets into the constants buffer
-  size_t D, Dt, DCD, cw, Qw, Pw, Rw, PhiE, PhiET, erow, ne, flag, eq, total;
+  size_t D, Dt, DCD, cw, Qw, Pw, Rw, PhiE, PhiET, erow, ne, flag, eq, eqr, total;
 };
 
 __host__ __device__ inline BigConst big_const_layout(int P, int M, int n, int p, int nc = 0) {
@@ -53,6 +53,7 @@ __host__ __device__ inline BigConst big_const_layout(int P, int M, int n, int p,
   L.ne = o;    o = align256(o + sizeof(int));               // E
   L.flag = o;  o = align256(o + sizeof(int) * Mr);          // scratch: row starts a new epoch
   L.eq = o;    o = align256(o + sizeof(int) * 2 * (nc > 0 ? nc : 1));  // equality-constraint index pairs
+  L.eqr = o;   o = align256(o + sizeof(double) * (nc > 0 ? nc : 1));   // their constants: v[a] - v[b] = r
   L.total = o;
   return L;
 }
@@ -121,6 +122,7 @@ struct BigArgs {
   double blb[8], bub[8];
   int nz, nc;        // extra variables / equality constraints (f4)
   double* Z;         // (B, nz) current extra variables (Z_out)
+  double* lam;       // (B, nc) or NULL: multipliers of the constraint rows, last bordered step
   unsigned long long tag;  // layout stamp expected at offset 0 of the constants buffer
   // component pairs (ca >= cb) of the measurement contraction, those whose G_e can be
   // nonzero first ("live": both components in the measurement Jacobian's support),
@@ -1291,12 +1293,14 @@ __global__ __launch_bounds__(BIG_NTHREADS, 2) void k_schol_back(BigArgs a) {
 
 // ------------------------------------------------------------ border (f4)
 // Bordered Gauss-Newton step for extra variables z and equality constraints
-// C v = 0 (include/mhe.h).  Runs after k_big_chol, which left the factor
+// C v = r (include/mhe.h; r = 0 for addEqConstraint rows, the bound or constant of
+// a row the host's active set imposes).  Runs after k_big_chol, which left the factor
 // H = L L^T (L_Ik tiles in place, L_kk^-T in LT) and the unconstrained step
 // du = -H^-1 g in YV.  With B = [H_xz  C^T] (dp x K), S = [H_zz 0; 0 0]:
 //   Z = H^-1 B                 (16-column panels: MFMA forward/backward substitution)
 //   (S - B^T Z) w = r - B^T du,  r = [-g_z ; -c(v)]
-//   dx = du - Z w,  dz = w[0:nz]
+//   dx = du - Z w,  dz = w[0:nz],  lambda = w[nz:K]  (H dx + C^T lambda = -g: the
+//   multipliers of L = J + lambda^T (C v - r), written to a.lam when given)
 // The Schur matrix is quasi-definite (z block SPD, constraint block negative
 // definite), so LDL^T without pivoting is stable; a z component no row depends on
 // (zero pivot with a zero row) is held fixed (dz = 0), the minimum-norm choice.
@@ -1316,6 +1320,7 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_border(BigArgs a) {
   double* ZM = ws + WL.ZM;
   const double* PhiE = (const double*)(a.cbuf + CL.PhiE);
   const int* eq = (const int*)(a.cbuf + CL.eq);
+  const double* eqr = (const double*)(a.cbuf + CL.eqr);
   const int E = a.M > 0 ? *(const int*)(a.cbuf + CL.ne) : 0;
   const int nz = a.nz, nc = a.nc, K = nz + nc, KP = (K + 15) / 16 * 16;
   const int NT = a.NT, Pp = a.Pp, dp = 16 * NT;
@@ -1435,7 +1440,7 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_border(BigArgs a) {
           for (int e = 0; e < E; ++e) base += ws[WL.GZVe + (size_t)e * NZX + r];
         } else {       // -c(v)
           const int ia = eq[2 * (r - nz)], ib = eq[2 * (r - nz) + 1];
-          base = -(X[ia] - (ib >= 0 ? X[ib] : 0.0));
+          base = -(X[ia] - (ib >= 0 ? X[ib] : 0.0) - eqr[r - nz]);
         }
         rw[r] = base - s;
       } else {
@@ -1485,6 +1490,8 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_border(BigArgs a) {
     YV[i] = s;
   }
   if (threadIdx.x < NZX) ws[WL.DZ + threadIdx.x] = threadIdx.x < nz ? rw[threadIdx.x] : 0.0;
+  if (a.lam)
+    for (int i = threadIdx.x; i < nc; i += BIG_NTHREADS) a.lam[(size_t)b * nc + i] = rw[nz + i];
 }
 
 // ------------------------------------------------------------ update

@@ -100,11 +100,14 @@ __global__ void k_big_consts(int P, int M, int n, int p, const double* D, const 
 // building constants stays a pure stream-ordered enqueue
 struct EqPairs {
   int v[2 * MHE_MAX_EQ];
+  double r[MHE_MAX_EQ];
 };
 __global__ void k_big_eq_consts(int P, int M, int n, int p, int nc, EqPairs e, char* cbuf) {
   const BigConst CL = big_const_layout(P, M, n, p, nc);
   int* o = (int*)(cbuf + CL.eq);
+  double* orr = (double*)(cbuf + CL.eqr);
   for (int i = threadIdx.x; i < 2 * nc; i += blockDim.x) o[i] = e.v[i];
+  for (int i = threadIdx.x; i < nc; i += blockDim.x) orr[i] = e.r[i];
 }
 
 // epoch detection: row i starts an epoch unless its Phi row equals row i-1 bitwise
@@ -249,6 +252,7 @@ int build_big_consts(const mhe_dims* dm, const double* D, const double* cw, cons
   if (dm->n_eq > 0) {
     EqPairs e = {};
     for (int i = 0; i < 2 * dm->n_eq; ++i) e.v[i] = dm->eq_idx[i];
+    for (int i = 0; i < dm->n_eq; ++i) e.r[i] = dm->eq_rhs ? dm->eq_rhs[i] : 0.0;
     hipLaunchKernelGGL(k_big_eq_consts, dim3(1), dim3(128), 0, st, P, dm->M, dm->n, dm->p, dm->n_eq, e, cbuf);
   }
   return hipGetLastError() == hipSuccess ? MHE_OK : MHE_ERR_HIP;
@@ -407,6 +411,7 @@ int mhe_solve(const mhe_dims* dims, const void* const_buf, const mhe_solve_args*
     A.nz = dims->n_extra;
     A.nc = dims->n_eq;
     A.Z = g->Z_out;
+    A.lam = dims->n_eq > 0 ? g->lambda_out : nullptr;
     A.huber = dims->dyn_cost == MHE_COST_HUBER;
     A.huber_delta = dims->huber_delta;
     A.tag = const_tag(dims, NT);

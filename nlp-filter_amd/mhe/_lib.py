@@ -36,7 +36,7 @@ class MheDims(_Sized):
         ("dyn_cost", c_i32), ("n_bounds", c_i32), ("huber_delta", c_dbl),
         ("bound_idx", c_i32 * 8), ("bound_lb", c_dbl * 8), ("bound_ub", c_dbl * 8),
         ("n_extra", c_i32), ("n_eq", c_i32), ("eq_idx", ctypes.POINTER(c_i32)),
-        ("force_large", c_i32), ("dyn_par", c_dbl * 8),
+        ("force_large", c_i32), ("dyn_par", c_dbl * 8), ("eq_rhs", ctypes.POINTER(c_dbl)),
     ]
 
 
@@ -55,7 +55,7 @@ class MheSolveArgs(_Sized):
                 ("U", c_vp), ("u_bstride", c_i64), ("Y", c_vp), ("PAR", c_vp), ("par_bstride", c_i64),
                 ("Rw", c_vp), ("rw_bstride", c_i64), ("x0", c_vp), ("cost_out", c_vp), ("iters_out", c_vp),
                 ("status_out", c_vp), ("max_iter", c_i32), ("tol", c_dbl), ("workspace", c_vp),
-                ("workspace_bytes", c_sz)]
+                ("workspace_bytes", c_sz), ("lambda_out", c_vp)]
 
 
 _P = ctypes.POINTER(MheDims)

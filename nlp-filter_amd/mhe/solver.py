@@ -64,8 +64,11 @@ class BatchSolver:
       dyn_cost        "l2" (weighted_l2_norm) or "huber" (pseudo_huber_loss, IRLS; huber_delta)
       bounds          [(state component, lb, ub), ...] enforced by projected Newton (addVarBounds)
       n_extra         extra decision variables z (meas="mixed" rows may reference them)
-      eq              (K, 2) equality constraints v[a] - v[b] = 0 on the node-major state
-                      vector (b = -1: v[a] = 0), met by every GN step (bordered KKT solve)
+      eq              (K, 2) equality constraints v[a] - v[b] = r on the node-major state
+                      vector (b = -1: v[a] = r), met by every GN step (bordered KKT solve);
+                      after each solve ``self.lam`` (B, K) holds their multipliers
+                      (L = J + lam^T (C v - r))
+      eq_rhs          (K,) the constants r (None: 0, the addEqConstraint rows)
       force_large     take the large-system path even when the register-resident kernel
                       fits (parity tests of the two paths; fixed at construction)
       dyn_par         static dynamics parameters (mhe_dims.dyn_par; registry.dyn_params turns a
@@ -78,7 +81,7 @@ class BatchSolver:
 
     def __init__(self, N, T, dyn, meas, D, cw, Phi, Qw, Rw, Pw=None, meas_idx=None, device="cuda",
                  dyn_cost="l2", huber_delta=None, bounds=None, n_extra=0, eq=None, force_large=False,
-                 dyn_par=None):
+                 dyn_par=None, eq_rhs=None):
         self.lib = _lib.load()
         if not torch.cuda.is_available():
             raise _lib.MheLibraryError("no HIP device visible: the estimator has no CPU path")
@@ -120,10 +123,16 @@ class BatchSolver:
         self._eq = np.zeros(0, dtype=np.int32) if eq is None else np.ascontiguousarray(
             np.asarray(eq, dtype=np.int32).reshape(-1, 2).ravel())
         dims.n_eq = self._eq.size // 2
+        self._eq_rhs = np.zeros(dims.n_eq) if eq_rhs is None else np.ascontiguousarray(
+            np.asarray(eq_rhs, dtype=np.float64).ravel())
+        if self._eq_rhs.size != dims.n_eq:
+            raise ValueError("eq_rhs needs one constant per equality row")
         if dims.n_eq:
             import ctypes
             dims.eq_idx = self._eq.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))  # self._eq keeps it alive
+            dims.eq_rhs = self._eq_rhs.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
         self.n_eq = dims.n_eq
+        self.lam = None
         dims.force_large = 1 if force_large else 0
         if dyn_par is None and dname == "vehicle_dynamics_and_gnss":
             raise ValueError("vehicle_dynamics_and_gnss needs dyn_par (registry.dyn_params(name, params))")
@@ -249,7 +258,7 @@ class BatchSolver:
         return t, (0 if t.shape[0] == 1 else int(np.prod(shape)))
 
     def _gn(self, s, cur, B, X, Xo, U_t, ustr, Y_t, PAR_t, pstr, x0_t, cost, iters, status, max_iter, tol,
-            Z=None, Zo=None, Rw=None):
+            Z=None, Zo=None, Rw=None, lam=None):
         Rw_t, rstr = self._rw(Rw, B)
         if B == 0:
             return
@@ -279,9 +288,10 @@ class BatchSolver:
             a.status_out = ctypes.c_void_p(status.data_ptr() + 4 * lo)
             a.max_iter, a.tol = int(max_iter), float(tol)
             a.workspace, a.workspace_bytes = (None if ws is None else ctypes.c_void_p(ws.data_ptr())), nb
+            a.lambda_out = at(lam, self.n_eq)
             rc = self.lib.mhe_solve(self.dims, _ptr(self.cbuf), ctypes.byref(a), _handle(s))
             _lib.check(rc, "mhe_solve")
-        keep_alive(s, cur, X, Xo, Z, Zo, U_t, Y_t, PAR_t, Rw_t, x0_t, cost, iters, status, ws)
+        keep_alive(s, cur, X, Xo, Z, Zo, U_t, Y_t, PAR_t, Rw_t, x0_t, cost, iters, status, ws, lam)
 
     # ------------------------------------------------------------------ calls
     def solve(self, X0, U, Y, PAR=None, x0=None, max_iter=20, tol=1e-10, stream=None, out=None, Z0=None, Rw=None):
@@ -304,8 +314,12 @@ class BatchSolver:
             if self.n_extra:
                 Z = _dev(np.zeros((B, self.n_extra)) if Z0 is None else Z0, self.device, (B, self.n_extra))
                 Zo = torch.empty_like(Z)
+            lam = None
+            if self.n_eq:
+                lam = torch.zeros((B, self.n_eq), dtype=torch.float64, device=self.device)
             self._gn(s, cur, B, X, Xo, U_t, ustr, Y_t, PAR_t, pstr, x0_t, cost, iters, status, max_iter, tol, Z, Zo,
-                     Rw)
+                     Rw, lam)
+            self.lam = lam
         if self.n_extra:
             return Xo, cost, iters, status, Zo
         return Xo, cost, iters, status

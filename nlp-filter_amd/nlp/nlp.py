@@ -35,8 +35,10 @@ Kept semantics
     every step.  Mixed rows carry scalar weights, so a full_state term in a mixed
     problem needs a diagonal R.
 
-Not on the Gauss-Newton path (raise ``UnsupportedFeature``): inequality
-constraints, equality-constraint plug-ins other than ``equality_constaint``,
+Inequality constraints (``addIneqConstraint``) and state bounds together with
+constraint rows are held by an active set over Gauss-Newton solves
+(``_solve_active_set``).  Not on the Gauss-Newton path (raise
+``UnsupportedFeature``): constraint plug-ins other than ``equality_constaint``,
 constraints on extra variables, and ``fixedTimeOptimalControlNLP`` (out of
 scope: the north star is the estimator).
 """
@@ -125,6 +127,8 @@ class NLP(object):
         self.solver = None
         self._bounds = []
         self._eq = []
+        self._ineq = []
+        self._active = []
 
     def addVariables(self, N_var, n_var, lb=None, ub=None, name='x'):
         X = []
@@ -142,19 +146,33 @@ class NLP(object):
     def addParameter(self, N_var, n_var, val=None):
         return [Param(n_var, val) for _ in range(N_var)]
 
+    @staticmethod
+    def _constraint_args(h, arguments, kind):
+        """The reference's constraint plug-in (nlp/constraints.py: equality_constaint,
+        args[0] - args[1]) on scalar elements ``X[i][k]`` of the state trajectory or one
+        element and a constant: (a, b) with at least one Elem."""
+        if _fname(h) != "equality_constaint":
+            raise UnsupportedFeature(f"{kind} constraint plug-in {_fname(h)!r}: supported is equality_constaint "
+                                     "(args[0] - args[1])")
+        args = list(arguments)
+        ok = len(args) == 2 and any(isinstance(a, Elem) for a in args) and all(
+            isinstance(a, Elem) or np.ndim(a) == 0 for a in args)
+        if not ok:
+            raise UnsupportedFeature("equality_constaint needs two scalar elements (or an element and a constant), "
+                                     "e.g. [X[i][2], X[i][7]]")
+        return tuple(a if isinstance(a, Elem) else float(a) for a in args)
+
     def addIneqConstraint(self, g, arguments, params=None):
-        raise UnsupportedFeature("inequality constraints are not on the Gauss-Newton path (SURVEY.md §8 f4)")
+        """nlp/nlp.py:49-50: g(arguments) <= 0 with g = equality_constaint, i.e.
+        args[0] <= args[1].  Enforced by an active set over Gauss-Newton solves:
+        active rows are held at equality by the bordered KKT step, their multipliers
+        decide release (see _solve_active_set)."""
+        self._ineq.append(self._constraint_args(g, arguments, "inequality"))
 
     def addEqConstraint(self, h, arguments, params=None):
         """nlp/nlp.py:52-53 with the reference's only equality plug-in,
-        constraints.equality_constaint (args[0] - args[1] == 0), on scalar
-        elements ``X[i][k]`` of the state trajectory."""
-        if _fname(h) != "equality_constaint":
-            raise UnsupportedFeature(f"equality constraint plug-in {_fname(h)!r}: supported is equality_constaint")
-        args = list(arguments)
-        if len(args) != 2 or not all(isinstance(a, Elem) for a in args):
-            raise UnsupportedFeature("equality_constaint needs two scalar variable elements, e.g. [X[i][2], X[i][7]]")
-        self._eq.append((args[0], args[1]))
+        constraints.equality_constaint (args[0] - args[1] == 0)."""
+        self._eq.append(self._constraint_args(h, arguments, "equality"))
 
     def setParameter(self, p, val):
         if not isinstance(p, Param):
@@ -356,8 +374,37 @@ class fixedTimeOptimalEstimationNLP(NLP):
                 return j * self.n + e.k
         raise UnsupportedFeature(f"constraint on {e!r}: only elements of the state trajectory are supported")
 
+    def _row(self, a, b):
+        """A constraint a - b (elements or constants) as (ia, ib, r, s): s (v[ia] - v[ib] - r)."""
+        if isinstance(a, Elem) and isinstance(b, Elem):
+            return self._state_index(a), self._state_index(b), 0.0, 1.0
+        if isinstance(a, Elem):
+            return self._state_index(a), -1, b, 1.0
+        return self._state_index(b), -1, a, -1.0
+
+    def _ineq_rows(self):
+        """Every inequality row s (v[ia] - v[ib] - r) <= 0: addIneqConstraint rows and, when
+        the problem also has constraint rows, the state bounds at every node (the device's
+        projected Newton handles bounds alone, not bounds together with a bordered step)."""
+        rows = [self._row(a, b) for a, b in self._ineq]
+        if rows or self._eq:
+            for c, lo, hi in self._enforced_bounds():
+                for j in range(self.N + 1):
+                    if np.isfinite(lo):
+                        rows.append((j * self.n + c, -1, lo, -1.0))
+                    if np.isfinite(hi):
+                        rows.append((j * self.n + c, -1, hi, 1.0))
+        return rows
+
     def _eq_pairs(self):
-        return np.array([(self._state_index(a), self._state_index(b)) for a, b in self._eq], dtype=np.int32)
+        """Equality rows for the device: the addEqConstraint rows, then the active set's."""
+        rows = [self._row(a, b)[:3] for a, b in self._eq]
+        ineq = self._ineq_rows() if self._active else []
+        rows += [ineq[i][:3] for i in self._active]
+        if not rows:
+            return None, None
+        return (np.array([(ia, ib) for ia, ib, _ in rows], dtype=np.int32),
+                np.array([r for _, _, r in rows], dtype=np.float64))
 
     def _mixed_rows(self, zoff):
         """MHE_MEAS_MIXED encoding (include/mhe.h) of every addResidualCost term:
@@ -507,9 +554,11 @@ class fixedTimeOptimalEstimationNLP(NLP):
         dyn_par = registry.dyn_params(dname, self._dyn[1]) if dname in registry.DYN else None
         Pw = None if self._prior is None else np.asarray(_resolve(self._prior[0]), dtype=np.float64)
         bounds = self._enforced_bounds()
+        if self._ineq or self._eq:
+            bounds = []   # held by the active set as constraint rows (_ineq_rows)
         huber = getattr(self, "_huber", None)
         extra, nz = self._extra_vars()
-        eq = self._eq_pairs() if self._eq else None
+        eq, eq_rhs = self._eq_pairs()
         general = self._is_general() or nz > 0
         if general:
             if nz > 4:
@@ -528,12 +577,12 @@ class fixedTimeOptimalEstimationNLP(NLP):
         linear = registry.MEAS[mname][3]
         key = (mname, t_meas.tobytes(), Rw.tobytes() if linear else Rw.shape, None if Pw is None else Pw.tobytes(),
                self._dyn_cost.tobytes(), huber, tuple(bounds), nz, None if eq is None else eq.tobytes(),
-               None if dyn_par is None else dyn_par.tobytes())
+               None if eq_rhs is None else eq_rhs.tobytes(), None if dyn_par is None else dyn_par.tobytes())
         if self._engine is None or self._engine_key != key:
             self._engine = _solver.BatchSolver(self.N, self.T, func, mname, self.CPM.D, (self.T / 2.0) * self.CPM.w,
                                                Phi, self._dyn_cost, Rw, Pw=Pw, meas_idx=idx, device=self.device,
                                                dyn_cost="huber" if huber is not None else "l2", huber_delta=huber,
-                                               bounds=bounds, n_extra=nz, eq=eq, dyn_par=dyn_par)
+                                               bounds=bounds, n_extra=nz, eq=eq, eq_rhs=eq_rhs, dyn_par=dyn_par)
             self._engine_key = key
             self.engine_builds = getattr(self, "engine_builds", 0) + 1
         self._Rw_solve = None if linear else Rw
@@ -547,10 +596,73 @@ class fixedTimeOptimalEstimationNLP(NLP):
         return self._engine
 
     # ------------------------------------------------------------ solve
+    MAX_ACTIVE_SET_STEPS = 60
+
     def solve(self, warmstart=False):
         """Gauss-Newton on the GPU (replaces opti.solve(), nlp/nlp.py:76-83)."""
         if warmstart and self.sol is not None:
             print('Warmstarting with previous solution')
+        if self._ineq or (self._eq and self._enforced_bounds()):
+            return self._solve_active_set(warmstart)
+        return self._solve_once(warmstart)
+
+    def _solve_active_set(self, warmstart):
+        """Inequality rows s (v[a] - v[b] - r) <= 0 by a primal active set over GN solves
+        (the KKT conditions IPOPT's interior point also reaches: feasibility, mu >= 0,
+        mu_i = 0 off the active set).  Each step solves the problem with the active rows
+        held at equality (bordered KKT step, multipliers lambda from the device:
+        L = J + lambda^T (C v - r), so mu = s lambda); then every violated inactive row
+        is added, or else the active row with the most negative mu is released.  The
+        start is the first solve's: rows violated at the initial iterate are active."""
+        rows = self._ineq_rows()
+        n_fixed = len(self._eq) + self._extra_vars()[1]
+        if n_fixed > 48:
+            raise UnsupportedFeature("more than 48 equality rows and extra variables")
+
+        def gvals():
+            v = np.concatenate([x.value if x.value is not None else (x.init if x.init is not None else
+                                np.zeros(self.n)) for x in self._X]).astype(np.float64)
+            return np.array([s_ * (v[ia] - (v[ib] if ib >= 0 else 0.0) - r) for ia, ib, r, s_ in rows])
+
+        if warmstart and self.sol is not None:
+            g0 = gvals()
+        else:
+            saved = [x.value for x in self._X]
+            for x in self._X:
+                x.value = None
+            g0 = gvals()
+            for x, v in zip(self._X, saved):
+                x.value = v
+        self._active = [i for i in np.argsort(-g0) if g0[i] > 0][:48 - n_fixed]
+        history = []
+        for step in range(self.MAX_ACTIVE_SET_STEPS):
+            self._solve_once(warmstart or step > 0, _quiet=True)
+            if not self.solver["success"]:
+                break
+            g = gvals()
+            scale = 1.0 + max(np.abs(x.value).max() for x in self._X)
+            lam = self._engine.lam.cpu().numpy()[0] if self._engine.lam is not None else np.zeros(0)
+            mu = np.array([rows[i][3] * lam[len(self._eq) + k] for k, i in enumerate(self._active)])
+            viol = [i for i in np.argsort(-g) if g[i] > 1e-9 * scale and i not in self._active]
+            history.append(len(self._active))
+            mu_tol = 1e-9 * (1.0 + (np.abs(lam).max() if lam.size else 0.0))
+            if viol:
+                room = 48 - n_fixed - len(self._active)
+                if room <= 0:
+                    raise UnsupportedFeature("active set needs more than 48 constraint rows")
+                self._active = self._active + viol[:room]
+            elif mu.size and mu.min() < -mu_tol:
+                self._active = [i for k, i in enumerate(self._active) if k != int(np.argmin(mu))]
+            else:
+                self.solver["active_set"] = [rows[i] for i in self._active]
+                self.solver["multipliers"] = mu
+                self.solver["active_set_steps"] = step + 1
+                return
+        warnings.warn("active set did not settle: returning the last Gauss-Newton solve")
+        self.solver["success"] = False
+        self.solver["active_set_steps"] = len(history)
+
+    def _solve_once(self, warmstart=False, _quiet=False):
         self._build()  # cheap when nothing changed; picks up re-set R / prior weights / params
         eng = self._engine
         P, n = self.N + 1, self.n
@@ -602,7 +714,7 @@ class fixedTimeOptimalEstimationNLP(NLP):
         self.solver = {"t_wall_total": t_wall, "iter_count": int(iters.cpu().numpy()[0]),
                        "return_status": statuses[st], "success": st == 0,
                        "objective": float(cost.cpu().numpy()[0]), "bounds_violated": self._check_bounds()}
-        if st != 0:
+        if st != 0 and not _quiet:
             warnings.warn(f"Gauss-Newton solve ended with {statuses[st]}")
 
     def _check_bounds(self):

@@ -15,7 +15,9 @@ Pinning: the constants (tau, D, w, poly1d phi) and the plug-in values/Jacobians
 are pinned against golden vectors produced by the reference itself
 (``tests/golden/gen_golden.py``, run in the build container where
 ``/root/reference`` exists); the EKF against the reference EKF run on the
-gnss_stationary log (``tests/golden/ekf_gnss_stationary.npz``, 51 steps, bit-exact);
+gnss_stationary log (``tests/golden/ekf_gnss_stationary.npz``, 51 steps, bit-exact)
+and against the reference EKF with autonomous-car.py's own plug-ins on 300 seeded steps
+(``tests/golden/ekf_autocar.npz``, 3e-14);
 the least-squares initialiser against reference runs on seeded logs and against the
 stored ``data/gnss-multi-receiver/LS_{A,B}.csv`` (tests/test_multi_receiver.py).  The
 stored result pickles (``ekf.pkl``, ``nlp-{l2,huber}.pkl``, ``nlp.pkl``) are NOT used:

@@ -91,12 +91,14 @@ def mixed_row(par, xt):
 class GeneralProblem(gn.Problem):
     """gn.Problem with meas = "mixed" rows (Rw (M,) scalar weights or (B, M)),
     ``n_extra`` extra variables and ``eq`` (K, 2) constraint index pairs into the
-    node-major state vector (second index -1: v[a] = 0)."""
+    node-major state vector: v[a] - v[b] = eq_rhs (second index -1: v[a] = eq_rhs;
+    eq_rhs None: 0)."""
 
-    def __init__(self, *args, n_extra=0, eq=None, **kw):
+    def __init__(self, *args, n_extra=0, eq=None, eq_rhs=None, **kw):
         super().__init__(*args, **kw)
         self.n_extra = int(n_extra)
         self.eq = np.zeros((0, 2), dtype=np.int64) if eq is None else np.asarray(eq, dtype=np.int64).reshape(-1, 2)
+        self.eq_rhs = np.zeros(self.eq.shape[0]) if eq_rhs is None else np.asarray(eq_rhs, dtype=np.float64).ravel()
 
 
 def _dynamics_part(pb, X, U, x0):
@@ -199,7 +201,7 @@ def gauss_newton_general(pb, X0, Z0, U, Y, PAR, x0=None, max_iter=20, tol=1e-10,
             if perturb is not None:
                 H, g = gn.perturb_rel(H, perturb), gn.perturb_rel(g, perturb + 1)
             v = np.concatenate([X[b].ravel(), Z[b]])
-            cval = C @ v
+            cval = C @ v - pb.eq_rhs
             try:
                 L = np.linalg.cholesky(H[0][:d, :d])
             except np.linalg.LinAlgError:
