@@ -37,6 +37,11 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 // waves per workgroup (one trajectory).  -DMHE_NW=16 builds the one-workgroup-per-CU
 // shape (5 slots per wave, 99 VGPRs, no scratch; bitwise-identical iterates) for A/B
 // runs -- measured 5 % slower at B = 128 and 256, 38 % at 1024
+// min waves per SIMD of the fused kernels' launch bounds: 4 = two 8-wave workgroups per
+// CU (128 VGPRs); 2 = one per CU with 256 VGPRs (A/B variant for small batches)
+#ifndef MHE_GN_MINW
+#define MHE_GN_MINW 4
+#endif
 #ifndef MHE_NW
 #define MHE_NW 8
 #endif
@@ -1481,7 +1486,7 @@ __device__ __forceinline__ int opaque_s(int x) {
 #define FSL smem_layout(opaque_s(a.P), opaque_s(a.M), n, opaque_s(a.NT), !MEAS::LINEAR)
 
 template <class DYN, class MEAS, int SLOTS, int mode, bool HUBER = false>
-__global__ __launch_bounds__(NTHREADS, 4) void k_gn(GnArgs a) {  // 2nd arg: min waves per SIMD (8 waves: 2 WGs per CU)
+__global__ __launch_bounds__(NTHREADS, MHE_GN_MINW) void k_gn(GnArgs a) {  // 2nd arg: min waves per SIMD (8 waves: 2 WGs per CU)
   constexpr int n = DYN::n;
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const ConstLayout CL = const_layout(a.P, a.M, n, MEAS::p, a.NT);
@@ -1676,7 +1681,7 @@ __device__ __forceinline__ double prior_cost(const GnArgs& a, const double* Pw, 
 #define FSLB smem_layout(opaque_s(a.P), opaque_s(a.M), n, opaque_s(a.NT), !MEAS::LINEAR, true)
 
 template <class DYN, class MEAS, int SLOTS, bool HUBER = false>
-__global__ __launch_bounds__(NTHREADS, 4) void k_gn_bounded(GnArgs a) {
+__global__ __launch_bounds__(NTHREADS, MHE_GN_MINW) void k_gn_bounded(GnArgs a) {
   constexpr int n = DYN::n;
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const SmemLayout SL = smem_layout(a.P, a.M, n, a.NT, !MEAS::LINEAR, true);
