@@ -756,6 +756,9 @@ constexpr int BIG_KB = 8;      // tile columns per super-block
 #define MHE_BIG_WIDE_NT 128
 #endif
 constexpr int BIG_WIDE_NT = MHE_BIG_WIDE_NT;
+#ifndef MHE_BIG_LLR8
+#define MHE_BIG_LLR8 2  // rows per wave of the left-looking update, 8-wide slab instance
+#endif
 #ifndef MHE_BIG_KO
 #define MHE_BIG_KO 0  // knock-out mask for timing probes only (tools/ko_big.sh): 1 trailing, 2 in-block, 4 TRSM
 #endif
@@ -790,7 +793,14 @@ __device__ __forceinline__ void stage_slab(double* LJ, const double* H, int J0, 
   }
 }
 
-template <int BIG_JB>
+// LL = true: LEFT-looking updates instead of the trailing update.  Before block column
+// k0 is factored, its tiles (I, k0 .. kend-1), I >= k0, receive all their updates
+// sum_{k < k0} L_Ik L_Jk^T in one visit: a wave keeps one row's BIG_JB accumulators in
+// registers while the block column's L_Jk are staged through LDS BIG_KB tile columns at
+// a time.  Every tile is then read and written ONCE per factorization (the right-looking
+// update reads and writes it once per super-block above it); L_Ik is read once per block
+// column (as before) and the staged L_Jk once per group of 8 rows.
+template <int BIG_JB, bool LL = false>
 __global__ __launch_bounds__(BIG_NTHREADS, BIG_JB == 8 ? 2 : 4) void k_big_chol(BigArgs a) {
   const int b = blockIdx.x;
   if (a.state[b] != BIG_RUNNING) return;
@@ -813,6 +823,98 @@ __global__ __launch_bounds__(BIG_NTHREADS, BIG_JB == 8 ? 2 : 4) void k_big_chol(
   init_units(UN);
   for (int k0 = 0; k0 < NT; k0 += BIG_KB) {
     const int kend = min(k0 + BIG_KB, NT);
+    if constexpr (LL) {
+      // ---- left-looking update of block column k0 by all previous columns: a wave
+      // takes LLR rows (g0 + wave + 8 q), so one staged slab serves 8 LLR rows
+      constexpr int LLR = BIG_JB == 8 ? MHE_BIG_LLR8 : 2;
+      for (int jh = 0; jh < kend - k0 && k0 > 0 && !(MHE_BIG_KO & 1); jh += BIG_JB) {
+        const int jw = min(BIG_JB, kend - k0 - jh), Jb = k0 + jh;
+        for (int g0 = Jb; g0 < NT; g0 += BIG_NW * LLR) {
+          int Iq[LLR], jm[LLR];
+          d4 c[LLR][BIG_JB];
+#pragma unroll
+          for (int q = 0; q < LLR; ++q) {
+            Iq[q] = g0 + wave + BIG_NW * q;
+            jm[q] = Iq[q] < NT ? min(jw, Iq[q] - Jb + 1) : 0;
+#pragma unroll
+            for (int jj = 0; jj < BIG_JB; ++jj) {
+              if (jj < jm[q]) {
+                const double* C = H + (size_t)big_tile_index(Iq[q], Jb + jj, NT) * 256;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) c[q][jj][r] = C[64 * r + lane];
+              }
+            }
+          }
+          for (int kc = 0; kc < k0; kc += BIG_KB) {
+            __syncthreads();  // the previous chunk's slab is consumed
+            stage_slab(LJ, H, Jb, jw, kc, BIG_KB, NT);  // L_Jk, jj < jw, kk < BIG_KB
+            __syncthreads();
+            // both rows share each staged B operand (one LDS read per 2 x 4 MFMAs); the
+            // rows' next L_Ik tiles are loaded one k step ahead
+            double av[LLR][4];
+#pragma unroll
+            for (int q = 0; q < LLR; ++q) {
+              const double* LI0 = H + (size_t)big_tile_index(jm[q] > 0 ? Iq[q] : Jb, kc, NT) * 256;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) av[q][r] = LI0[64 * r + lane];  // negated by the MFMA
+            }
+#pragma unroll 1
+            for (int kk = 0; kk < BIG_KB; ++kk) {
+              double an[LLR][4];
+#pragma unroll
+              for (int q = 0; q < LLR; ++q) {
+                const double* LIn =
+                    H + (size_t)big_tile_index(jm[q] > 0 ? Iq[q] : Jb, kc + min(kk + 1, BIG_KB - 1), NT) * 256;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) an[q][r] = LIn[64 * r + lane];
+              }
+#pragma unroll
+              for (int jj = 0; jj < BIG_JB; ++jj) {
+                if (jj < jm[0]) {  // rows ascend with q: jm[0] <= jm[1]
+                  const double* Bt = LJ + (jj * BIG_KB + kk) * 256;
+                  double bv[4];
+#pragma unroll
+                  for (int r = 0; r < 4; ++r) bv[r] = Bt[64 * r + lane];
+#pragma unroll
+                  for (int q = 0; q < LLR; ++q) {
+                    if (jj < jm[q]) {
+#pragma unroll
+                      for (int r = 0; r < 4; ++r)
+                        c[q][jj] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[q][r], bv[r], c[q][jj], 0, 0, MFMA_NEG_A);
+                    }
+                  }
+                } else if (jj < jm[LLR - 1]) {
+                  const double* Bt = LJ + (jj * BIG_KB + kk) * 256;
+                  double bv[4];
+#pragma unroll
+                  for (int r = 0; r < 4; ++r) bv[r] = Bt[64 * r + lane];
+#pragma unroll
+                  for (int r = 0; r < 4; ++r)
+                    c[LLR - 1][jj] =
+                        __builtin_amdgcn_mfma_f64_16x16x4f64(av[LLR - 1][r], bv[r], c[LLR - 1][jj], 0, 0, MFMA_NEG_A);
+                }
+              }
+#pragma unroll
+              for (int q = 0; q < LLR; ++q)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) av[q][r] = an[q][r];
+            }
+          }
+#pragma unroll
+          for (int q = 0; q < LLR; ++q) {
+#pragma unroll
+            for (int jj = 0; jj < BIG_JB; ++jj) {
+              if (jj < jm[q]) {
+                double* C = H + (size_t)big_tile_index(Iq[q], Jb + jj, NT) * 256;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) C[64 * r + lane] = c[q][jj][r];
+              }
+            }
+          }
+        }
+      }
+      __syncthreads();  // the block column is up to date; LJ is free for LB / LTs
+    }
     // ---- diagonal block, left-looking inside the block column: at step k every tile
     // (I, k), k <= I < kend, gets all of its in-block updates in ONE pass (K = 16 (k - k0),
     // L_kk' operands from LDS), then the TRSM.  Two workgroup barriers per k.
@@ -930,8 +1032,8 @@ __global__ __launch_bounds__(BIG_NTHREADS, BIG_JB == 8 ? 2 : 4) void k_big_chol(
       }
     }
     __syncthreads();
-    // ---- trailing update with K = (kend - k0) tiles
-    for (int J0 = kend; J0 < NT && !(MHE_BIG_KO & 1); J0 += BIG_JB) {
+    // ---- trailing update with K = (kend - k0) tiles (right-looking form only)
+    for (int J0 = kend; J0 < NT && !LL && !(MHE_BIG_KO & 1); J0 += BIG_JB) {
       const int jb = min(BIG_JB, NT - J0);
       stage_slab(LJ, H, J0, jb, k0, kb, NT);  // L_Jk (jb x kb tiles) into LDS
       __syncthreads();
