@@ -760,7 +760,8 @@ constexpr int BIG_WIDE_NT = MHE_BIG_WIDE_NT;
 #define MHE_BIG_LLR8 2  // rows per wave of the left-looking update, 8-wide slab instance
 #endif
 #ifndef MHE_BIG_KO
-#define MHE_BIG_KO 0  // knock-out mask for timing probes only (tools/ko_big.sh): 1 trailing, 2 in-block, 4 TRSM
+#define MHE_BIG_KO 0  // knock-out mask for timing probes only (tools/ko_big.sh): 1 trailing / left-looking
+                      // update, 2 in-block, 4 TRSM, 8 the left-looking update's slab staging
 #endif
 constexpr int BIG_LB_TILES = BIG_KB * (BIG_KB - 1) / 2;
 // the LJ region: the trailing slab, or (panel phase) the in-block L tiles LB and the
@@ -847,7 +848,7 @@ __global__ __launch_bounds__(BIG_NTHREADS, BIG_JB == 8 ? 2 : 4) void k_big_chol(
           }
           for (int kc = 0; kc < k0; kc += BIG_KB) {
             __syncthreads();  // the previous chunk's slab is consumed
-            stage_slab(LJ, H, Jb, jw, kc, BIG_KB, NT);  // L_Jk, jj < jw, kk < BIG_KB
+            if (!(MHE_BIG_KO & 8)) stage_slab(LJ, H, Jb, jw, kc, BIG_KB, NT);  // L_Jk, jj < jw, kk < BIG_KB
             __syncthreads();
             // both rows share each staged B operand (one LDS read per 2 x 4 MFMAs); the
             // rows' next L_Ik tiles are loaded one k step ahead
