@@ -1004,32 +1004,67 @@ __global__ __launch_bounds__(BIG_NTHREADS, BIG_JB == 8 ? 2 : 4) void k_big_chol(
     // without barriers; the row's L_Ik' are re-read right after this wave wrote them
     // (L2 hits: the old form re-read them after a sweep over every row)
     const int kb = kend - k0;
-    for (int I = kend + wave; I < NT; I += BIG_NW) {
+    // 8-wide instance: two rows per wave (I, I + 8), independent MFMA chains and their
+    // L_Ik' loads in flight together, the block's L_kk' read once from LDS for both (C4
+    // +2 %, C5 +0.7 %); the 4-wide one keeps one row per wave (the second row's registers
+    // spill there: C3 -0.9 %).  Unused second-row work is dead code at JB = 4.
+    constexpr int RPW = BIG_JB == 8 ? 2 : 1;
+    for (int I = kend + wave; I < NT; I += RPW * BIG_NW) {
+      const bool two = RPW == 2 && I + BIG_NW < NT;
+      const int I2 = two ? I + BIG_NW : I;
       for (int kk = 0; kk < kb; ++kk) {
         double* Ak = H + (size_t)big_tile_index(I, k0 + kk, NT) * 256;
-        d4 c;
+        double* Ak2 = H + (size_t)big_tile_index(I2, k0 + kk, NT) * 256;
+        d4 c, c2;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) c[r] = Ak[(lane & 15) * 16 + 4 * r + (lane >> 4)];
+        for (int r = 0; r < 4; ++r) {
+          c[r] = Ak[(lane & 15) * 16 + 4 * r + (lane >> 4)];
+          c2[r] = Ak2[(lane & 15) * 16 + 4 * r + (lane >> 4)];
+        }
         for (int kp = 0; kp < kk && !(MHE_BIG_KO & 2); ++kp) {
           const double* Lk = LB + (kk * (kk - 1) / 2 + kp) * 256;
           const double* LI = H + (size_t)big_tile_index(I, k0 + kp, NT) * 256;
+          const double* LI2 = H + (size_t)big_tile_index(I2, k0 + kp, NT) * 256;
+          double lk[4], li[4], li2[4];
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
-            c = __builtin_amdgcn_mfma_f64_16x16x4f64(Lk[64 * r + lane], LI[64 * r + lane], c, 0, 0, MFMA_NEG_A);
+          for (int r = 0; r < 4; ++r) {
+            lk[r] = Lk[64 * r + lane];
+            li[r] = LI[64 * r + lane];
+            li2[r] = LI2[64 * r + lane];
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            c = __builtin_amdgcn_mfma_f64_16x16x4f64(lk[r], li[r], c, 0, 0, MFMA_NEG_A);
+            c2 = __builtin_amdgcn_mfma_f64_16x16x4f64(lk[r], li2[r], c2, 0, 0, MFMA_NEG_A);
+          }
         }
         const double* LT = LTs + kk * DTS;
-        d4 t = {0.0, 0.0, 0.0, 0.0};
+        d4 t = {0.0, 0.0, 0.0, 0.0}, t2 = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          t = __builtin_amdgcn_mfma_f64_16x16x4f64(LT[(4 * r + (lane >> 4)) * LIS + (lane & 15)], c[r], t, 0, 0, 0);
+        for (int r = 0; r < 4; ++r) {
+          const double lv = LT[(4 * r + (lane >> 4)) * LIS + (lane & 15)];
+          t = __builtin_amdgcn_mfma_f64_16x16x4f64(lv, c[r], t, 0, 0, 0);
+          t2 = __builtin_amdgcn_mfma_f64_16x16x4f64(lv, c2[r], t2, 0, 0, 0);
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r) Ak[64 * r + lane] = t[r];
+        if (two) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) Ak2[64 * r + lane] = t2[r];
+        }
         const int k = k0 + kk;
-        double s = t[0] * YV[16 * k + (lane >> 4)] + t[1] * YV[16 * k + 4 + (lane >> 4)] +
-                   t[2] * YV[16 * k + 8 + (lane >> 4)] + t[3] * YV[16 * k + 12 + (lane >> 4)];
+        const double y0 = YV[16 * k + (lane >> 4)], y1 = YV[16 * k + 4 + (lane >> 4)],
+                     y2 = YV[16 * k + 8 + (lane >> 4)], y3 = YV[16 * k + 12 + (lane >> 4)];
+        double s = t[0] * y0 + t[1] * y1 + t[2] * y2 + t[3] * y3;
+        double s2 = t2[0] * y0 + t2[1] * y1 + t2[2] * y2 + t2[3] * y3;
         s += __shfl_xor(s, 16);
         s += __shfl_xor(s, 32);
-        if (lane < 16) BV[16 * I + lane] -= s;
+        s2 += __shfl_xor(s2, 16);
+        s2 += __shfl_xor(s2, 32);
+        if (lane < 16) {
+          BV[16 * I + lane] -= s;
+          if (two) BV[16 * I2 + lane] -= s2;
+        }
       }
     }
     __syncthreads();
