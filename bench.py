@@ -1,20 +1,23 @@
 """Benchmark: Gauss-Newton collocation-point updates/sec (BASELINE.json metric).
 
-Workload (BASELINE.json configs[1]): van der Pol (nlp/dynamics.py:61-66),
-full_state measurements, N=100 (P=101 CGL nodes), T=10, M=101, batch 1024
-independent trajectories per GPU (weak scaling: each rank solves its own
-seeded shard; the only collectives are the one-time RCCL broadcast of the
-model constants and the max-over-ranks of the elapsed time).
+Workload (BASELINE.json configs[1] and north star): van der Pol
+(nlp/dynamics.py:61-66), full_state measurements, N=100 (P=101 CGL nodes), T=10,
+M=101, ONE seeded batch of 1024 independent trajectories split over the G GPUs
+(strong scaling, the north star's "batch-1024 at 1, 2, 4 and 8 MI355X"): rank r
+generates only its contiguous shard [r*1024/G, (r+1)*1024/G) of that batch
+(configs.make_c2(shard=...), bitwise the slice of the full batch), rank 0 builds
+the model constants and the other ranks RECEIVE them by one RCCL broadcast
+(setup, untimed); the only other collectives are the max-over-ranks of the elapsed
+time and the sum of the iteration counts.  ``--weak`` gives every rank its own
+seeded batch of ``--batch`` trajectories instead (weak scaling).
 
-One step = one mhe_gn_solve launch over the resident batch doing exactly
-GN_ITERS full Gauss-Newton iterations per trajectory (tol = 0): residual +
-Jacobian, J^T W J / J^T W r assembly, register-tiled Cholesky, two triangular
-solves, update.  value = (all ranks) B * P * GN_ITERS * K / max-rank wall.
+One step = one mhe_solve launch over the resident shard doing exactly GN_ITERS
+full Gauss-Newton iterations per trajectory (tol = 0): residual + Jacobian,
+J^T W J / J^T W r assembly, register-tiled Cholesky, two triangular solves,
+update.  value = (all ranks) sum of B_r * P * GN_ITERS * K / max-rank wall.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu] [--global-batch G]
-N > 1 is launched by torch.distributed.run (RANK/LOCAL_RANK/WORLD_SIZE env).  Default:
-weak scaling (1024 trajectories per GPU); --global-batch 1024 splits one fixed batch
-over the ranks (strong scaling, "scaling": "strong").
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu] [--global-batch G] [--weak [--batch B]]
+N > 1 is launched by torch.distributed.run (RANK/LOCAL_RANK/WORLD_SIZE env).
 """
 import argparse
 import json
@@ -118,15 +121,28 @@ def cpu_baseline(w, iters, sample_B, target_s=10.0):
                       f"thread"}
 
 
+def rank_workload(world, rank, global_batch=1024, weak=False, batch=1024, N=100):
+    """The C2 trajectories rank `rank` of `world` solves.  Strong (default): its
+    contiguous shard of ONE seeded batch of `global_batch` (seed 1), generated alone;
+    weak: its own seeded batch of `batch` (seed 1 + 1000 rank).  tests/test_dist_gloo.py
+    checks that the shards of the strong split are the full batch, bitwise."""
+    from mhe import configs, dist
+    if weak:
+        return configs.make_c2(B=batch, seed=dist.shard_seed(1, rank), N=N)
+    return configs.make_c2(B=global_batch, seed=1, N=N, shard=dist.shard_range(global_batch, world, rank))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=1024, help="trajectories per GPU (weak scaling)")
-    ap.add_argument("--global-batch", type=int, default=None,
-                    help="strong scaling: this many trajectories in total, split over the ranks "
-                         "(dist.shard_range); the north star's fixed batch-1024 at 1/2/4/8 GPUs")
+    ap.add_argument("--global-batch", type=int, default=1024,
+                    help="strong scaling (default): this many trajectories in total, split over the "
+                         "ranks (dist.shard_range) -- the north star's fixed batch-1024 at 1/2/4/8 GPUs")
+    ap.add_argument("--weak", action="store_true",
+                    help="weak scaling instead: --batch trajectories per GPU, a seeded batch per rank")
+    ap.add_argument("--batch", type=int, default=1024, help="trajectories per GPU with --weak")
     ap.add_argument("--iters", type=int, default=GN_ITERS)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=1024)
@@ -144,18 +160,14 @@ def main():
     torch.cuda.set_device(dev)
     dist.init("nccl", dev)
 
-    if args.global_batch:
-        # strong scaling: one global problem set (seed 1), rank r solves its contiguous shard
-        lo, hi = dist.shard_range(args.global_batch, world, rank)
-        w = configs.make_c2(B=args.global_batch, seed=1)
-        for k in ("X_init", "Y", "X_true"):
-            setattr(w, k, getattr(w, k)[lo:hi])
-        w.B = hi - lo
-    else:
-        w = configs.make_c2(B=args.batch, seed=dist.shard_seed(1, rank))
-    s = solver.from_workload(w, device=dev)
-    # model constants: rank 0's device buffer broadcast over RCCL/xGMI (one-time, untimed)
+    w = rank_workload(world, rank, args.global_batch, args.weak, args.batch)
+    # model constants: built once on rank 0; the other ranks only allocate the buffer and
+    # receive rank 0's bytes over RCCL/xGMI (one-time, untimed).  The kernels check the
+    # buffer's layout stamp against their own dims before using it.
+    s = solver.from_workload(w, device=dev, constants="build" if rank == 0 else "receive")
     dist.broadcast_(s.cbuf, src=0)
+    if rank != 0:
+        s.constants_ready()
     staged = s.prepare(w.X_init, w.U, w.Y)
     B = w.B
     outs = (torch.empty_like(staged[0]), torch.empty(B, dtype=torch.float64, device=dev),
@@ -198,12 +210,13 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": wall / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "strong" if args.global_batch else "weak",
+            "scaling": "weak" if args.weak else "strong",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (seeded van der Pol truth via RK4 + Gaussian noise, R/Q from estimation_example.py)",
             "config": {"workload": "C2 van_der_pol: n=2, m=1, full_state p=2, N=100 (P=101, d=202), T=10, M=101",
-                       "global_batch": args.global_batch or B * world, "batch_per_gpu": B,
+                       "global_batch": B * world if args.weak else args.global_batch,
+                       "batch_per_gpu": B,  # rank 0's (strong: its shard_range of the global batch)
                        "gn_iters_per_step": args.iters,
                        "parallelism": f"dp{world} (independent trajectories; RCCL broadcast of constants only)"},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",

@@ -138,7 +138,10 @@ typedef struct mhe_dims {
                            (nlp/nlp.py:52-53, nlp/constraints.py): v[a] - v[b] = 0 */
   const int32_t* eq_idx;/* HOST pointer, 2*n_eq entries (a, b) into the flattened
                            state vector v = X (P*n, node-major: j*n + c); b = -1
-                           means v[a] = 0.  Copied into the constants buffer.     */
+                           means v[a] = 0.  Copied into the constants buffer at
+                           build time and part of its layout stamp (with eq_rhs):
+                           solving with other rows than the buffer was built with
+                           returns MHE_STATUS_BAD_CONSTANTS -- rebuild instead.     */
   int32_t force_large;  /* 1: take the large-system path even when the problem fits
                            the register-resident kernel (parity tests of the two
                            paths on identical inputs).  The path is a function of
@@ -171,6 +174,19 @@ typedef struct mhe_dims {
  * a small quasi-definite LDL^T of the Schur complement).  Linear constraints are
  * therefore met exactly after every step.  Bounds and constraints together are
  * not supported (MHE_ERR_UNSUPPORTED). */
+
+/* Process-wide A/B options, for measurements and tests only; nothing else (no
+ * environment variable) changes what a solve runs.  Returns the previous value, or
+ * MHE_ERR_DIMS for an unknown option or a value out of range.
+ *   MHE_OPT_BIG_RIGHT_LOOKING  1: the large-system factorization's right-looking
+ *                              trailing-update form (bitwise-identical iterates,
+ *                              slower); 0 (default): left-looking block columns
+ *   MHE_OPT_DEBUG_SMEM_PAD     bytes of LDS added to the fused kernel's launch
+ *                              (forces lower occupancy; default 0)
+ * Not thread-safe against concurrent launches: set it before enqueueing work. */
+#define MHE_OPT_BIG_RIGHT_LOOKING 1
+#define MHE_OPT_DEBUG_SMEM_PAD 2
+int32_t mhe_set_option(int32_t option, int32_t value);
 
 /* Size in bytes of the device constants buffer for `dims` (0 on bad dims).  The
  * first 256 bytes are a header holding the layout stamp written by

@@ -1156,279 +1156,6 @@ __global__ __launch_bounds__(BIG_NTHREADS, BIG_JB == 8 ? 2 : 4) void k_big_chol(
   }
 }
 
-// ------------------------------------------------------------ split factorization
-// The same right-looking super-blocked Cholesky as k_big_chol, as three launches per
-// super-block of BIG_SKB = 16 tile columns over ALL trajectories, so that several CUs
-// work on one trajectory and share its block column through their XCD's L2:
-//   k_schol_diag   one workgroup per trajectory: the 16 x 16-tile diagonal block
-//                  (single-wave panels, in-block left-looking updates, TRSM, y_k);
-//   k_schol_rows   one wave per row below the block (8 rows per workgroup): A_Ik read
-//                  once, in-block updates and TRSM, L_Ik written once, b_I -= L_Ik y_k;
-//   k_schol_trail  ROW-STATIONARY trailing update: a workgroup takes 8 consecutive rows,
-//                  each wave keeps its row's 16 L_Ik tiles in VGPRs (read once) and walks
-//                  the column slabs J <= I, the slab's L_Jk (4 x 16 tiles, 128 KB) staged
-//                  in LDS.  The row groups of one trajectory run on one XCD (block ids
-//                  b + 8 t share an XCD) and stage the same slabs at about the same time:
-//                  L2 serves the repeats.  Every trailing tile is read and written once
-//                  per 256 columns (k_big_chol: per 128) and no L tile is re-read per slab
-//                  from HBM.
-//   k_schol_back   one workgroup per trajectory: the backward solve.
-// Cross-workgroup data moves only across launches (stream order).
-constexpr int BIG_SKB = 16;  // tile columns per super-block
-constexpr int BIG_SJB = 4;   // tile columns per trailing slab (LDS: 4 x 16 tiles)
-__host__ __device__ constexpr int big_schol_trail_lds() { return BIG_SJB * BIG_SKB * 256; }      // doubles
-__host__ __device__ constexpr int big_schol_rows_lds() { return BIG_SKB * DTS; }                 // doubles
-__host__ __device__ constexpr int big_schol_diag_lds() { return DTS + UNITS + 2; }              // doubles
-
-// (trajectory, sub-block) of this workgroup: block ids g + 8 t (one XCD under the
-// observed round-robin placement; speed only) take trajectories g + 8 (t / nsub)
-__device__ __forceinline__ void xcd_split(int nsub, int& b, int& r) {
-  const int L = blockIdx.x, t = L >> 3;
-  b = (L & 7) + 8 * (t / nsub);
-  r = t % nsub;
-}
-
-template <int KB>
-__global__ __launch_bounds__(BIG_NTHREADS, 2) void k_schol_diag(BigArgs a, int k0) {
-  const int b = blockIdx.x;
-  if (a.state[b] != BIG_RUNNING) return;
-  const BigWs WL = big_ws_layout(a.P, a.M, a.n, a.NT, a.nz, a.nc);
-  double* ws = a.ws + (size_t)b * a.ws_stride;
-  double* H = ws + WL.H;
-  double* LTg = ws + WL.LT;
-  double* BV = ws + WL.BV;
-  double* YV = ws + WL.YV;
-  extern __shared__ __attribute__((aligned(16))) double sm[];
-  double* DT = sm;               // DTS: A_kk, then L_kk^-T
-  double* UN = sm + DTS;         // identity rows for the panel (unit_row)
-  int* flag = (int*)(UN + UNITS);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int NT = a.NT, kend = min(k0 + KB, NT);
-  if (threadIdx.x == 0) *flag = 0;
-  init_units(UN);
-  for (int k = k0; k < kend; ++k) {
-    const int nk = k - k0;
-    if (wave == 0) {
-      // diagonal tile: A_kk - sum L_kk' L_kk'^T -> DT, panel, y_k
-      const double* Akk = H + (size_t)big_tile_index(k, k, NT) * 256;
-      d4 c;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) c[r] = Akk[64 * r + lane];
-      for (int kk = 0; kk < nk; ++kk) {
-        const double* Lt = H + (size_t)big_tile_index(k, k0 + kk, NT) * 256;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const double v = Lt[64 * r + lane];
-          c = __builtin_amdgcn_mfma_f64_16x16x4f64(v, v, c, 0, 0, MFMA_NEG_A);
-        }
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) DT[64 * r + lane] = c[r];
-      wave_lds_sync();
-      const bool bad = panel(DT, UN, lane);
-      if (bad && lane == 0) *flag = 1;
-      wave_lds_sync();
-      block_fwd(DT, BV + 16 * k, YV + 16 * k, lane);  // y_k = L_kk^-1 b_k
-      for (int e = lane; e < DTS; e += 64) LTg[(size_t)k * DTS + e] = DT[e];
-    } else {
-      // block rows k < I < kend: c' = A_Ik^T - sum_k' L_kk' L_Ik'^T, stored k-major in place
-      for (int I = k + wave; I < kend; I += BIG_NW - 1) {
-        double* Ak = H + (size_t)big_tile_index(I, k, NT) * 256;
-        d4 c;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) c[r] = Ak[(lane & 15) * 16 + 4 * r + (lane >> 4)];
-        for (int kk = 0; kk < nk; ++kk) {
-          const double* Lk = H + (size_t)big_tile_index(k, k0 + kk, NT) * 256;
-          const double* LI = H + (size_t)big_tile_index(I, k0 + kk, NT) * 256;
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            c = __builtin_amdgcn_mfma_f64_16x16x4f64(Lk[64 * r + lane], LI[64 * r + lane], c, 0, 0, MFMA_NEG_A);
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) Ak[64 * r + lane] = c[r];
-      }
-    }
-    __syncthreads();
-    if (*flag) break;
-    // TRSM: L_Ik^T = L_kk^-1 A_Ik^T (k-major result) for the block rows, b_I -= L_Ik y_k
-    const double yk = YV[16 * k + (lane >> 4)], yk1 = YV[16 * k + 4 + (lane >> 4)],
-                 yk2 = YV[16 * k + 8 + (lane >> 4)], yk3 = YV[16 * k + 12 + (lane >> 4)];
-    for (int I = k + 1 + wave; I < kend; I += BIG_NW) {
-      double* Ak = H + (size_t)big_tile_index(I, k, NT) * 256;
-      double av[4], bv[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        av[r] = DT[(4 * r + (lane >> 4)) * LIS + (lane & 15)];  // L_kk^-1 [lane & 15][4r + (lane >> 4)]
-        bv[r] = Ak[64 * r + lane];
-      }
-      d4 u = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int r = 0; r < 4; ++r) u = __builtin_amdgcn_mfma_f64_16x16x4f64(av[r], bv[r], u, 0, 0, 0);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) Ak[64 * r + lane] = u[r];
-      double s = u[0] * yk + u[1] * yk1 + u[2] * yk2 + u[3] * yk3;
-      s += __shfl_xor(s, 16);
-      s += __shfl_xor(s, 32);
-      if (lane < 16) BV[16 * I + lane] -= s;
-    }
-    __syncthreads();
-  }
-  if (*flag && threadIdx.x == 0) a.state[b] = MHE_STATUS_NOT_SPD;
-}
-
-template <int KB>
-__global__ __launch_bounds__(BIG_NTHREADS, 2) void k_schol_rows(BigArgs a, int k0, int nsub, int batch) {
-  int b, rg;
-  xcd_split(nsub, b, rg);
-  if (b >= batch || a.state[b] != BIG_RUNNING) return;
-  const BigWs WL = big_ws_layout(a.P, a.M, a.n, a.NT, a.nz, a.nc);
-  double* ws = a.ws + (size_t)b * a.ws_stride;
-  double* H = ws + WL.H;
-  const double* LTg = ws + WL.LT;
-  double* BV = ws + WL.BV;
-  const double* YV = ws + WL.YV;
-  extern __shared__ __attribute__((aligned(16))) double sm[];
-  double* LTs = sm;  // the block's L_kk^-T
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int NT = a.NT, kend = min(k0 + KB, NT), kb = kend - k0;
-  for (int e = threadIdx.x; e < kb * DTS; e += BIG_NTHREADS) LTs[e] = LTg[(size_t)k0 * DTS + e];
-  __syncthreads();
-  const int I = kend + 8 * rg + wave;
-  if (I >= NT) return;
-  // the same operations per element as the diagonal block's rows (in-block updates in
-  // k' order, TRSM, b_I update in k order); the row's L_Ik' are re-read right after
-  // this wave wrote them, the block's L_kk' are shared by every row (L2)
-  for (int kk = 0; kk < kb; ++kk) {
-    double* Ak = H + (size_t)big_tile_index(I, k0 + kk, NT) * 256;
-    d4 c;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) c[r] = Ak[(lane & 15) * 16 + 4 * r + (lane >> 4)];
-    for (int kp = 0; kp < kk; ++kp) {
-      const double* Lk = H + (size_t)big_tile_index(k0 + kk, k0 + kp, NT) * 256;
-      const double* LI = H + (size_t)big_tile_index(I, k0 + kp, NT) * 256;
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        c = __builtin_amdgcn_mfma_f64_16x16x4f64(Lk[64 * r + lane], LI[64 * r + lane], c, 0, 0, MFMA_NEG_A);
-    }
-    const double* LT = LTs + kk * DTS;
-    d4 t = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-      t = __builtin_amdgcn_mfma_f64_16x16x4f64(LT[(4 * r + (lane >> 4)) * LIS + (lane & 15)], c[r], t, 0, 0, 0);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) Ak[64 * r + lane] = t[r];
-    const int k = k0 + kk;
-    double s = t[0] * YV[16 * k + (lane >> 4)] + t[1] * YV[16 * k + 4 + (lane >> 4)] +
-               t[2] * YV[16 * k + 8 + (lane >> 4)] + t[3] * YV[16 * k + 12 + (lane >> 4)];
-    s += __shfl_xor(s, 16);
-    s += __shfl_xor(s, 32);
-    if (lane < 16) BV[16 * I + lane] -= s;
-  }
-}
-
-template <int KB, int JB>
-__global__ __launch_bounds__(BIG_NTHREADS, 2) void k_schol_trail(BigArgs a, int k0, int nsub, int batch) {
-  // launched only for super-blocks with rows below them, which are always full (KB
-  // columns): a partial super-block is the last one
-  int b, rg;
-  xcd_split(nsub, b, rg);
-  if (b >= batch || a.state[b] != BIG_RUNNING) return;
-  const BigWs WL = big_ws_layout(a.P, a.M, a.n, a.NT, a.nz, a.nc);
-  double* H = a.ws + (size_t)b * a.ws_stride + WL.H;
-  extern __shared__ __attribute__((aligned(16))) double sm[];
-  double* LJ = sm;  // staged L_Jk tiles [jj][kk][256]
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int NT = a.NT, kend = k0 + KB;
-  const int I0 = kend + 8 * rg, I = I0 + wave, Ilast = min(I0 + 7, NT - 1);
-  // this wave's row: L_Ik for the block's k in registers (A operands, negated by the MFMA)
-  double la[KB][4];
-  {
-    const int Ic = I < NT ? I : NT - 1;
-#pragma unroll
-    for (int kk = 0; kk < KB; ++kk) {
-      const double* LI = H + (size_t)big_tile_index(Ic, k0 + kk, NT) * 256;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) la[kk][r] = LI[64 * r + lane];
-    }
-  }
-  for (int J0 = kend; J0 <= Ilast; J0 += JB) {
-    const int jb = min(JB, NT - J0);
-    __syncthreads();  // the previous slab is consumed
-    stage_slab(LJ, H, J0, jb, k0, KB, NT);
-    __syncthreads();
-    if (I < NT && I >= J0) {
-      // one tile at a time: a chain of 4 KB MFMAs per tile (one wave keeps its SIMD's
-      // MFMA pipe busy at 64 of every 66 cycles), no accumulators beside the row's L_I
-      const int jmax = min(jb, I - J0 + 1);
-      d4 cn;  // the next tile's C, loaded one tile ahead (its HBM latency under this tile's chain)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) cn[r] = H[(size_t)big_tile_index(I, J0, NT) * 256 + 64 * r + lane];
-      for (int jj = 0; jj < jmax; ++jj) {
-        double* C = H + (size_t)big_tile_index(I, J0 + jj, NT) * 256;
-        d4 c = cn;
-        if (jj + 1 < jmax) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) cn[r] = H[(size_t)big_tile_index(I, J0 + jj + 1, NT) * 256 + 64 * r + lane];
-        }
-        const double* Bj = LJ + jj * KB * 256 + lane;
-#pragma unroll
-        for (int kk = 0; kk < KB; ++kk) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            c = __builtin_amdgcn_mfma_f64_16x16x4f64(la[kk][r], Bj[kk * 256 + 64 * r], c, 0, 0, MFMA_NEG_A);
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) C[64 * r + lane] = c[r];
-      }
-    }
-  }
-}
-
-// backward solve after the split factorization: delta_k = L_kk^-T (y_k - sum_{I>k} L_Ik^T delta_I)
-template <int KB>
-__global__ __launch_bounds__(BIG_NTHREADS, 2) void k_schol_back(BigArgs a) {
-  const int b = blockIdx.x;
-  if (a.state[b] != BIG_RUNNING) return;
-  const BigWs WL = big_ws_layout(a.P, a.M, a.n, a.NT, a.nz, a.nc);
-  double* ws = a.ws + (size_t)b * a.ws_stride;
-  const double* H = ws + WL.H;
-  const double* LTg = ws + WL.LT;
-  double* YV = ws + WL.YV;
-  __shared__ double DT[DTS];
-  __shared__ double PART[BIG_NW * 16];
-  __shared__ double YL[16];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int NT = a.NT;
-  for (int k = NT - 1; k >= 0; --k) {
-    double pv = 0.0;
-    for (int I = k + 1 + wave; I < NT; I += BIG_NW) {
-      const double* L = H + (size_t)big_tile_index(I, k, NT) * 256;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int tr = (lane >> 4) + 4 * r;
-        pv += L[(lane & 15) * 16 + tr] * YV[16 * I + tr];  // L_Ik[tr][lane & 15], k-major tile
-      }
-    }
-    pv += __shfl_xor(pv, 16);
-    pv += __shfl_xor(pv, 32);
-    if (lane < 16) PART[wave * 16 + lane] = pv;
-    __syncthreads();
-    if (wave == 0) {
-      if (lane < 16) {
-        double rhs = YV[16 * k + lane];
-        for (int w = 0; w < BIG_NW; ++w) rhs -= PART[w * 16 + lane];
-        YL[lane] = rhs;
-      }
-      for (int e = lane; e < DTS; e += 64) DT[e] = LTg[(size_t)k * DTS + e];
-      wave_lds_sync();
-      block_back(DT, YL, lane);
-      wave_lds_sync();
-      if (lane < 16) YV[16 * k + lane] = YL[lane];
-    }
-    __syncthreads();
-  }
-}
-
 // ------------------------------------------------------------ border (f4)
 // Bordered Gauss-Newton step for extra variables z and equality constraints
 // C v = r (include/mhe.h; r = 0 for addEqConstraint rows, the bound or constant of

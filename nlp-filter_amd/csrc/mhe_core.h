@@ -56,6 +56,12 @@ constexpr int MAX_SLOTS = (MAX_NT * (MAX_NT - 1) / 2 + NW - 1) / NW;  // 10 at 8
 
 enum Mode { MODE_SOLVE = 0, MODE_ASSEMBLE = 1, MODE_LINSOLVE = 2 };
 
+// Process-wide A/B options (defined in mhe_gn.hip, set only through the explicit
+// mhe_set_option call of include/mhe.h -- never from the environment): the
+// right-looking large-path factorization and an LDS pad that forces occupancy.
+extern int g_opt_big_right_looking;
+extern int g_opt_smem_pad;
+
 // ------------------------------------------------------------ layouts
 struct ConstLayout {
   size_t D, Dt, Phi, PhiT, cw, Qw, Pw, Rw, Cc, DA, DB, DAc, DBc, total;  // byte offsets
@@ -2048,8 +2054,7 @@ int launch_gn(const mhe_dims* dm, GnArgs& a, int batch, int mode, hipStream_t st
     return MHE_ERR_UNSUPPORTED;  // mixed rows: large-system path only
   } else {
     const bool bounded = mode == MODE_SOLVE && dm->n_bounds > 0;
-    int smem = smem_bytes(dm, a.NT, bounded);
-    if (const char* pad = getenv("MHE_DEBUG_SMEM_PAD")) smem += atoi(pad);  // debug: force occupancy
+    const int smem = smem_bytes(dm, a.NT, bounded) + g_opt_smem_pad;  // pad: mhe_set_option, occupancy A/B only
     if (smem > REG_LDS_LIMIT) return MHE_ERR_UNSUPPORTED;
     void (*kern)(GnArgs) = nullptr;
     const bool huber = dm->dyn_cost == MHE_COST_HUBER;
@@ -2086,25 +2091,12 @@ int launch_big(const mhe_dims* dm, BigArgs& A, int batch, int max_iter, hipStrea
   const bool wide = A.NT >= BIG_WIDE_NT;
   const int smem = big_chol_lds(wide ? 8 : 4) * (int)sizeof(double);
   // left-looking block-column updates (default; 38 % less HBM traffic than the
-  // right-looking trailing update, C3 +5 %, C4 +7.5 %, C5 +8 %); MHE_BIG_LL=0 selects the
-  // right-looking form for A/B runs
-  const char* el = getenv("MHE_BIG_LL");
-  const bool ll = el ? atoi(el) != 0 : true;
+  // right-looking trailing update, C3 +5 %, C4 +7.5 %, C5 +8 %); the right-looking form
+  // (bitwise-identical iterates, tests/test_gpu_big.py) only when a caller selected it
+  // explicitly with mhe_set_option(MHE_OPT_BIG_RIGHT_LOOKING, 1)
+  const bool ll = g_opt_big_right_looking == 0;
   void (*chol)(BigArgs) = wide ? (ll ? k_big_chol<8, true> : k_big_chol<8>) : (ll ? k_big_chol<4, true> : k_big_chol<4>);
   if (hipFuncSetAttribute((const void*)chol, hipFuncAttributeMaxDynamicSharedMemorySize, smem) != hipSuccess)
-    return MHE_ERR_HIP;
-  // split factorization (k_schol_*, several CUs per trajectory: 2.7x less HBM traffic but
-  // 9-13 % slower than k_big_chol); MHE_BIG_SPLIT=1 selects it (A/B runs)
-  const char* es = getenv("MHE_BIG_SPLIT");
-  const bool split = es ? atoi(es) != 0 : false;
-  const int smem_sd = big_schol_diag_lds() * (int)sizeof(double), smem_sr = big_schol_rows_lds() * (int)sizeof(double),
-            smem_st = big_schol_trail_lds() * (int)sizeof(double);
-  if (split && (hipFuncSetAttribute((const void*)k_schol_diag<BIG_SKB>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    smem_sd) != hipSuccess ||
-                hipFuncSetAttribute((const void*)k_schol_rows<BIG_SKB>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    smem_sr) != hipSuccess ||
-                hipFuncSetAttribute((const void*)k_schol_trail<BIG_SKB, BIG_SJB>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, smem_st) != hipSuccess))
     return MHE_ERR_HIP;
   const int K = A.nz + A.nc;
   const int smem_b = (K * K + 2 * K) * (int)sizeof(double);
@@ -2124,22 +2116,7 @@ int launch_big(const mhe_dims* dm, BigArgs& A, int batch, int max_iter, hipStrea
   for (int it = 0; it < max_iter; ++it) {
     hipLaunchKernelGGL((k_big_resid<DYN, MEAS>), dim3(batch), dim3(BIG_NTHREADS), 0, st, A, 0);
     hipLaunchKernelGGL((k_big_assemble<DYN, MEAS>), dim3((npos * A.nch + 3) / 4, batch), dim3(256), 0, st, A);
-    if (split) {
-      for (int k0 = 0; k0 < A.NT; k0 += BIG_SKB) {
-        hipLaunchKernelGGL(k_schol_diag<BIG_SKB>, dim3(batch), dim3(BIG_NTHREADS), smem_sd, st, A, k0);
-        const int below = A.NT - min(k0 + BIG_SKB, A.NT);
-        if (below > 0) {
-          const int nsub = (below + 7) / 8;  // 8 rows per workgroup
-          const dim3 grid((unsigned)(8 * ((batch + 7) / 8) * nsub));
-          hipLaunchKernelGGL(k_schol_rows<BIG_SKB>, grid, dim3(BIG_NTHREADS), smem_sr, st, A, k0, nsub, batch);
-          hipLaunchKernelGGL((k_schol_trail<BIG_SKB, BIG_SJB>), grid, dim3(BIG_NTHREADS), smem_st, st, A, k0, nsub,
-                             batch);
-        }
-      }
-      hipLaunchKernelGGL(k_schol_back<BIG_SKB>, dim3(batch), dim3(BIG_NTHREADS), 0, st, A);
-    } else {
-      hipLaunchKernelGGL(chol, dim3(batch), dim3(BIG_NTHREADS), smem, st, A);
-    }
+    hipLaunchKernelGGL(chol, dim3(batch), dim3(BIG_NTHREADS), smem, st, A);
     if (K > 0) hipLaunchKernelGGL((k_big_border<DYN::n, MEAS::p>), dim3(batch), dim3(BIG_NTHREADS), smem_b, st, A);
     if (bounded)
       hipLaunchKernelGGL((k_big_linesearch<DYN, MEAS>), dim3(batch), dim3(BIG_NTHREADS), smem_ls, st, A);

@@ -19,6 +19,8 @@
 // tile registers.  Trajectories are independent: no inter-workgroup traffic.
 //
 // See DESIGN.md for the data layout, the roofline and the measurements.
+#include <string.h>
+
 #include "mhe_core.h"
 
 namespace mhe {
@@ -154,6 +156,9 @@ __global__ void k_big_epoch_rows(int P, int M, int n, int p, const double* Phi, 
 
 __global__ void k_write_tag(unsigned long long* p, unsigned long long tag) { *p = tag; }
 
+int g_opt_big_right_looking = 0;
+int g_opt_smem_pad = 0;
+
 }  // namespace mhe
 
 // ================================================================ dispatch
@@ -225,14 +230,26 @@ size_t const_total_bytes(const mhe_dims* dm, int NT) {
   return const_layout(dm->N + 1, dm->M, dm->n, dm->p, NT).total;
 }
 
-// FNV-1a over the dims that define the constants' layout and contents
+// FNV-1a over the dims that define the constants' layout and contents, including the
+// equality rows (eq_idx pairs and the bits of eq_rhs), which mhe_build_constants copies
+// into the buffer: a solve whose dims carry other rows than the buffer was built with
+// is refused (MHE_STATUS_BAD_CONSTANTS) instead of silently using the old rows.
 unsigned long long const_tag(const mhe_dims* dm, int NT) {
   unsigned long long h = 1469598103934665603ull;
-  const long long v[] = {0x4D4845, is_big(dm) ? 1 : 0, dm->N, dm->n, dm->m, dm->p, dm->M, dm->q, dm->dyn_model,
-                         dm->meas_model, dm->has_prior, dm->dyn_cost, NT, dm->n_eq, dm->n_extra};
-  for (long long x : v) {
+  auto mix = [&h](long long x) {
     h ^= (unsigned long long)x;
     h *= 1099511628211ull;
+  };
+  const long long v[] = {0x4D4845, is_big(dm) ? 1 : 0, dm->N, dm->n, dm->m, dm->p, dm->M, dm->q, dm->dyn_model,
+                         dm->meas_model, dm->has_prior, dm->dyn_cost, NT, dm->n_eq, dm->n_extra};
+  for (long long x : v) mix(x);
+  if (dm->n_eq > 0 && dm->eq_idx)  // check_dims has validated n_eq <= MHE_MAX_EQ and eq_idx
+    for (int i = 0; i < 2 * dm->n_eq; ++i) mix(dm->eq_idx[i]);
+  for (int i = 0; i < dm->n_eq; ++i) {  // NULL eq_rhs = all 0 (as the build); -0 and +0 alike
+    const double r = (dm->eq_rhs ? dm->eq_rhs[i] : 0.0) + 0.0;
+    long long bits;
+    memcpy(&bits, &r, sizeof bits);
+    mix(bits);
   }
   return h | 1ull;
 }
@@ -292,6 +309,16 @@ extern "C" void mhe_diag_set_buffer(void* p) { g_dbg = (unsigned long long*)p; }
 #endif
 
 extern "C" {
+
+int32_t mhe_set_option(int32_t option, int32_t value) {
+  int* slot = option == MHE_OPT_BIG_RIGHT_LOOKING ? &g_opt_big_right_looking
+              : option == MHE_OPT_DEBUG_SMEM_PAD  ? &g_opt_smem_pad
+                                                  : nullptr;
+  if (!slot || value < 0 || (option == MHE_OPT_DEBUG_SMEM_PAD && value > 160 * 1024)) return MHE_ERR_DIMS;
+  const int old = *slot;
+  *slot = value;
+  return old;
+}
 
 const char* mhe_version(void) { return "libmhe 0.3 (gfx950, register-tiled fp64 MFMA Cholesky)"; }
 

@@ -14,6 +14,7 @@ LIB_PATH = os.environ.get("MHE_LIB", os.path.join(HERE, "libmhe.so"))
 MHE_OK = 0
 ERRORS = {-1: "MHE_ERR_DIMS", -2: "MHE_ERR_MODEL", -3: "MHE_ERR_HIP", -4: "MHE_ERR_UNSUPPORTED", -5: "MHE_ERR_NULL"}
 STATUS = {0: "converged", 1: "max_iter", 2: "not_spd", 3: "nonfinite", 4: "bad_constants"}
+OPT_BIG_RIGHT_LOOKING, OPT_DEBUG_SMEM_PAD = 1, 2  # mhe_set_option (A/B runs and tests only)
 
 # symbol -> (restype, argtypes); must match include/mhe.h exactly
 c_i32, c_i64, c_dbl, c_vp, c_sz = ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p, ctypes.c_size_t
@@ -63,6 +64,7 @@ _PE = ctypes.POINTER(MheEkfDims)
 _PL = ctypes.POINTER(MheLsDims)
 SIGNATURES = {
     "mhe_version": (ctypes.c_char_p, []),
+    "mhe_set_option": (c_i32, [c_i32, c_i32]),
     "mhe_padded_dim": (c_i32, [_P]),
     "mhe_const_bytes": (c_sz, [_P]),
     "mhe_build_constants": (ctypes.c_int, [_P, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),

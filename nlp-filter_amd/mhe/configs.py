@@ -90,17 +90,27 @@ def vdp_rhs(t, x):
     return np.stack([(1 - x[:, 1] ** 2) * x[:, 0] - x[:, 1], x[:, 0]], axis=1)
 
 
-def make_c2(B=1024, seed=1, N=100):
+def make_c2(B=1024, seed=1, N=100, shard=None):
+    """C2.  ``shard=(lo, hi)``: only trajectories [lo, hi) of the seeded batch of B --
+    bitwise the same arrays as slicing the full batch (the random draws are made for
+    all B, in batch order, which costs microseconds; the RK4 truth and the initial
+    iterates, the expensive part, only for the shard).  The strong-scaling bench
+    gives every rank its own shard this way (mhe.dist.shard_range)."""
     T, M = 10.0, 101
+    lo, hi = (0, B) if shard is None else (int(shard[0]), int(shard[1]))
+    if not 0 <= lo <= hi <= B:
+        raise ValueError(f"shard {shard} outside [0, {B}]")
     rng = np.random.default_rng(seed)
-    x0 = np.array([0.0, 1.0])[None, :] + rng.normal(size=(B, 2)) * 0.1
+    x0 = (np.array([0.0, 1.0])[None, :] + rng.normal(size=(B, 2)) * 0.1)[lo:hi]
     t = np.linspace(0, T, M)
     xt = _rk4(vdp_rhs, x0, t)
     R = np.diag([0.01, 0.02])
-    Y = xt + rng.normal(size=xt.shape) * np.sqrt(np.diag(R))[None, None, :]
+    noise = rng.normal(size=(B, M, 2))[lo:hi]
+    Y = xt + noise * np.sqrt(np.diag(R))[None, None, :]
     cpm = ChebyshevPseudospectralMethod(N, 0, T)
     Q = np.diag([1e-4, 1e-4])
-    return Workload(name="C2_van_der_pol", N=N, T=T, n=2, m=1, p=2, M=M, B=B,
+    B = hi - lo
+    return Workload(name="C2_van_der_pol", N=N, T=T, n=2, m=1, p=2, M=M, B=B, shard=(lo, hi),
                     dyn="van_der_pol", meas="full_state", meas_static={},
                     t_meas=t, Y=Y, U=np.zeros((1, N + 1, 1)), PAR=None, Qw=np.linalg.inv(Q),
                     Rw=np.broadcast_to(np.linalg.inv(R), (M, 2, 2)).copy(), Pw=None, x0=None,

@@ -73,6 +73,9 @@ class BatchSolver:
                       fits (parity tests of the two paths; fixed at construction)
       dyn_par         static dynamics parameters (mhe_dims.dyn_par; registry.dyn_params turns a
                       plug-in's params dict into it, e.g. car_params for vehicle_dynamics_and_gnss)
+      constants       "build" (default): build the device constants here; "receive": only
+                      allocate ``cbuf`` -- a data-parallel rank > 0 receives rank 0's bytes
+                      (mhe.dist.broadcast_) and then calls constants_ready()
     With meas="mixed", PAR rows follow include/mhe.h (q = 14) and Rw is (M,) weights.
     """
 
@@ -81,7 +84,7 @@ class BatchSolver:
 
     def __init__(self, N, T, dyn, meas, D, cw, Phi, Qw, Rw, Pw=None, meas_idx=None, device="cuda",
                  dyn_cost="l2", huber_delta=None, bounds=None, n_extra=0, eq=None, force_large=False,
-                 dyn_par=None, eq_rhs=None):
+                 dyn_par=None, eq_rhs=None, constants="build"):
         self.lib = _lib.load()
         if not torch.cuda.is_available():
             raise _lib.MheLibraryError("no HIP device visible: the estimator has no CPU path")
@@ -148,20 +151,42 @@ class BatchSolver:
         if nbytes == 0:
             raise _lib.MheCallError("mhe_const_bytes: invalid dims")
         dev = self.device
-        self._host = dict(D=np.asarray(D, np.float64), cw=np.asarray(cw, np.float64), Phi=Phi,
-                          Qw=np.asarray(Qw, np.float64), Rw=np.asarray(Rw, np.float64).reshape(self.M, p, p),
-                          Pw=None if Pw is None else np.asarray(Pw, np.float64))
-        self._src = {k: _dev(v, dev) for k, v in self._host.items() if v is not None}
         self.cbuf = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-        Pw_t = self._src.get("Pw")
         self._ws = collections.OrderedDict()  # large-system workspace per stream handle (LRU, <= WS_CACHE)
+        self._built = torch.cuda.Event()  # launches on any stream wait for the constants
+        if constants == "receive":
+            # another process builds the buffer (rank 0 of a data-parallel job); the caller
+            # fills self.cbuf (mhe.dist.broadcast_) and then calls constants_ready()
+            self._ready = False
+            return
+        if constants != "build":
+            raise ValueError(f"constants must be 'build' or 'receive', got {constants!r}")
+        self._ready = True
+        src = dict(D=np.asarray(D, np.float64), cw=np.asarray(cw, np.float64), Phi=Phi,
+                   Qw=np.asarray(Qw, np.float64), Rw=np.asarray(Rw, np.float64).reshape(self.M, p, p),
+                   Pw=None if Pw is None else np.asarray(Pw, np.float64))
+        src = {k: _dev(v, dev) for k, v in src.items() if v is not None}
         cur = torch.cuda.current_stream(dev)
         rc = self.lib.mhe_build_constants(
-            self.dims, _ptr(self._src["D"]), _ptr(self._src["cw"]), _ptr(self._src["Phi"]),
-            _ptr(self._src["Qw"]), _ptr(self._src["Rw"]), _ptr(Pw_t), _ptr(self.cbuf), _handle(cur))
+            self.dims, _ptr(src["D"]), _ptr(src["cw"]), _ptr(src["Phi"]),
+            _ptr(src["Qw"]), _ptr(src["Rw"]), _ptr(src.get("Pw")), _ptr(self.cbuf), _handle(cur))
         _lib.check(rc, "mhe_build_constants")
-        self._built = torch.cuda.Event()  # launches on any stream wait for the constants
+        # the staging tensors may be freed now: the build reads them on `cur`, where the
+        # caching allocator orders their reuse
         self._built.record(cur)
+
+    def constants_ready(self, stream=None):
+        """A solver built with constants="receive": self.cbuf now holds the bytes another
+        process built for the same dims (enqueued on ``stream``, default the current one);
+        later launches on any stream wait for that point.  A buffer built for other dims
+        is refused per trajectory by the kernels' layout stamp (MHE_STATUS_BAD_CONSTANTS)."""
+        s = torch.cuda.current_stream(self.device) if stream is None else stream
+        self._built.record(s)
+        self._ready = True
+
+    def _check_ready(self):
+        if not self._ready:
+            raise _lib.MheCallError("constants not received yet: fill cbuf and call constants_ready()")
 
     # ------------------------------------------------------------------ inputs
     def _inputs(self, X, U, Y, PAR, x0):
@@ -200,18 +225,22 @@ class BatchSolver:
         mhe_gn_solve_ws then needs a device workspace (allocated here, cached)."""
         return self.lib.mhe_workspace_bytes(self.dims, 1) > 0
 
-    def _chunk(self, B):
+    def _chunk(self, B, s=None):
         """Trajectories per launch on the large-system path: all B unless their
         workspace exceeds the budget (ws_budget bytes, default 85 % of the free HBM
-        plus what this solver already holds) -- then the batch is streamed in equal
-        chunks through one workspace (C5: 2048 trajectories x 0.28 GB)."""
+        plus the workspace this solver holds for stream ``s``, which the launch
+        replaces) -- then the batch is streamed in equal chunks through one workspace
+        (C5: 2048 trajectories x 0.28 GB).  Workspaces cached for OTHER streams stay
+        allocated (a launch there may still be using them), so they are not counted
+        as free."""
         per = self.lib.mhe_workspace_bytes(self.dims, 1)
         if per == 0 or B == 0:
             return B
         budget = self.ws_budget
         if budget is None:
             free, _ = torch.cuda.mem_get_info(self.device)
-            budget = int(0.85 * (free + sum(w.numel() for w in self._ws.values())))
+            own = self._ws.get(s.cuda_stream) if s is not None else None
+            budget = int(0.85 * (free + (own.numel() if own is not None else 0)))
         k = max(1, min(B, budget // per))
         if k >= B:
             return B
@@ -262,7 +291,7 @@ class BatchSolver:
         Rw_t, rstr = self._rw(Rw, B)
         if B == 0:
             return
-        chunk = self._chunk(B)
+        chunk = self._chunk(B, s)
         ws, nb = self._workspace(chunk, s)
         P, n, M = self.P, self.n, self.M
         for lo in range(0, B, chunk):
@@ -294,13 +323,18 @@ class BatchSolver:
         keep_alive(s, cur, X, Xo, Z, Zo, U_t, Y_t, PAR_t, Rw_t, x0_t, cost, iters, status, ws, lam)
 
     # ------------------------------------------------------------------ calls
-    def solve(self, X0, U, Y, PAR=None, x0=None, max_iter=20, tol=1e-10, stream=None, out=None, Z0=None, Rw=None):
+    def solve(self, X0, U, Y, PAR=None, x0=None, max_iter=20, tol=1e-10, stream=None, out=None, Z0=None, Rw=None,
+              lam_out=None):
         """Gauss-Newton to convergence. Returns (X, cost, iters, status) device tensors,
         and the extra variables Z (B, n_extra) as a fifth element when n_extra > 0.
         ``Rw`` (B|1, M, p, p) -- (B|1, M) for mixed rows -- replaces the measurement
         weights of the constants for this solve (nonlinear models; the MHE windows'
         R = 0 slot masks).  With ``stream`` the work (staging included) is ordered on
-        that stream; consume the outputs there or make the consuming stream wait for it."""
+        that stream; consume the outputs there or make the consuming stream wait for it.
+        ``lam_out`` (B, n_eq) float64 device tensor: receives this solve's constraint
+        multipliers (the per-call way; ``self.lam`` is the last solve's on any stream,
+        kept for single-stream callers)."""
+        self._check_ready()
         with launch_stream(stream, self.device, (self._built,)) as (s, cur):
             X, B, U_t, ustr, Y_t, PAR_t, pstr, x0_t = self._inputs(X0, U, Y, PAR, x0)
             if out is None:
@@ -316,7 +350,13 @@ class BatchSolver:
                 Zo = torch.empty_like(Z)
             lam = None
             if self.n_eq:
-                lam = torch.zeros((B, self.n_eq), dtype=torch.float64, device=self.device)
+                if lam_out is not None:
+                    if tuple(lam_out.shape) != (B, self.n_eq) or lam_out.dtype != torch.float64:
+                        raise ValueError(f"lam_out must be float64 ({B}, {self.n_eq})")
+                    lam = lam_out
+                    lam.zero_()
+                else:
+                    lam = torch.zeros((B, self.n_eq), dtype=torch.float64, device=self.device)
             self._gn(s, cur, B, X, Xo, U_t, ustr, Y_t, PAR_t, pstr, x0_t, cost, iters, status, max_iter, tol, Z, Zo,
                      Rw, lam)
             self.lam = lam
@@ -331,12 +371,14 @@ class BatchSolver:
     def solve_staged(self, staged, outs, max_iter, tol, stream=None):
         X, B, U_t, ustr, Y_t, PAR_t, pstr, x0_t = staged
         Xo, cost, iters, status = outs
+        self._check_ready()
         with launch_stream(stream, self.device, (self._built,)) as (s, cur):
             self._gn(s, cur, B, X, Xo, U_t, ustr, Y_t, PAR_t, pstr, x0_t, cost, iters, status, max_iter, tol)
 
     def resjac(self, X, U, Y, PAR=None, stream=None):
         """Per-node defects W (B,P,n) and dynamics Jacobians F (B,P,n,n), per-row
         residuals E (B,M,p) and measurement Jacobians Hm (B,M,p,n) at X (mhe_resjac)."""
+        self._check_ready()
         with launch_stream(stream, self.device, (self._built,)) as (s, cur):
             X, B, U_t, ustr, Y_t, PAR_t, pstr, _ = self._inputs(X, U, Y, PAR, np.zeros((X.shape[0], self.n))
                                                                 if self.dims.has_prior else None)
@@ -353,6 +395,7 @@ class BatchSolver:
 
     def assemble(self, X, U, Y, PAR=None, x0=None, stream=None):
         """GN normal equations at X: H (B,dp,dp), g (B,dp), cost (B)."""
+        self._check_ready()
         with launch_stream(stream, self.device, (self._built,)) as (s, cur):
             X, B, U_t, ustr, Y_t, PAR_t, pstr, x0_t = self._inputs(X, U, Y, PAR, x0)
             H = torch.empty((B, self.dp, self.dp), dtype=torch.float64, device=self.device)
@@ -366,6 +409,7 @@ class BatchSolver:
 
     def chol_solve(self, H, g, stream=None):
         """delta = -H^{-1} g with the solver's tiled Cholesky (H: (B,dp,dp) SPD)."""
+        self._check_ready()
         with launch_stream(stream, self.device, (self._built,)) as (s, cur):
             H = _dev(H, self.device)
             g = _dev(g, self.device)

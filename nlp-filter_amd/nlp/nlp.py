@@ -166,7 +166,11 @@ class NLP(object):
         """nlp/nlp.py:49-50: g(arguments) <= 0 with g = equality_constaint, i.e.
         args[0] <= args[1].  Enforced by an active set over Gauss-Newton solves:
         active rows are held at equality by the bordered KKT step, their multipliers
-        decide release (see _solve_active_set)."""
+        decide release (see _solve_active_set).  Row cap: the device's bordered step
+        holds at most 48 rows -- equality rows + extra variables + ACTIVE inequality
+        rows, where a state bound next to constraint rows counts one row per node.
+        More than that raises UnsupportedFeature (before any solve when the start
+        already violates too many rows)."""
         self._ineq.append(self._constraint_args(g, arguments, "inequality"))
 
     def addEqConstraint(self, h, arguments, params=None):
@@ -633,15 +637,26 @@ class fixedTimeOptimalEstimationNLP(NLP):
             g0 = gvals()
             for x, v in zip(self._X, saved):
                 x.value = v
-        self._active = [i for i in np.argsort(-g0) if g0[i] > 0][:48 - n_fixed]
+        start_active = [i for i in np.argsort(-g0) if g0[i] > 0]
+        if len(start_active) > 48 - n_fixed:
+            # the device's bordered step holds at most 48 rows (equality rows + extra
+            # variables + active inequality rows): refuse before any solve, not midway
+            raise UnsupportedFeature(f"{len(start_active)} inequality rows (bounds next to constraint rows count one "
+                                     f"per node) are violated at the start; at most {48 - n_fixed} can be held "
+                                     f"active beside {n_fixed} equality rows and extra variables")
+        self._active = start_active
         history = []
         for step in range(self.MAX_ACTIVE_SET_STEPS):
-            self._solve_once(warmstart or step > 0, _quiet=True)
+            lam_t = self._solve_once(warmstart or step > 0, _quiet=True)
             if not self.solver["success"]:
-                break
+                # an inner Gauss-Newton failure is the result: keep its status
+                warnings.warn(f"active set step {step}: Gauss-Newton solve ended with "
+                              f"{self.solver['return_status']}")
+                self.solver["active_set_steps"] = step + 1
+                return
             g = gvals()
             scale = 1.0 + max(np.abs(x.value).max() for x in self._X)
-            lam = self._engine.lam.cpu().numpy()[0] if self._engine.lam is not None else np.zeros(0)
+            lam = lam_t.cpu().numpy()[0] if lam_t is not None else np.zeros(0)
             mu = np.array([rows[i][3] * lam[len(self._eq) + k] for k, i in enumerate(self._active)])
             viol = [i for i in np.argsort(-g) if g[i] > 1e-9 * scale and i not in self._active]
             history.append(len(self._active))
@@ -691,7 +706,10 @@ class fixedTimeOptimalEstimationNLP(NLP):
         import torch
         t0 = time.perf_counter()
         Rw = None if self._Rw_solve is None else self._Rw_solve[None]
-        out = eng.solve(X0, U, Y, PAR, x0, max_iter=self.max_iter, tol=self.tol, Z0=Z0, Rw=Rw)
+        lam_t = None
+        if eng.n_eq:
+            lam_t = torch.empty((1, eng.n_eq), dtype=torch.float64, device=eng.device)
+        out = eng.solve(X0, U, Y, PAR, x0, max_iter=self.max_iter, tol=self.tol, Z0=Z0, Rw=Rw, lam_out=lam_t)
         X, cost, iters, status = out[:4]
         torch.cuda.synchronize()
         t_wall = time.perf_counter() - t0
@@ -716,6 +734,7 @@ class fixedTimeOptimalEstimationNLP(NLP):
                        "objective": float(cost.cpu().numpy()[0]), "bounds_violated": self._check_bounds()}
         if st != 0 and not _quiet:
             warnings.warn(f"Gauss-Newton solve ended with {statuses[st]}")
+        return lam_t
 
     def _check_bounds(self):
         viol = False

@@ -142,8 +142,13 @@ def meas_eval(name, x, par=None, static=None):
         rho = np.sqrt(d[..., 0] ** 2 + d[..., 1] ** 2 + d[..., 2] ** 2)
         h = (rho + x[..., idx[3]])[..., None]
         H = np.zeros(x.shape[:-1] + (1, n))
+        # rho = 0 only at a placeholder satellite slot (position 0, weight 0: the rows
+        # the solves mask, autonomous-car.py:260-263): its line-of-sight row is left 0
+        # instead of 0/0 = NaN, so the checker never relies on masking a NaN away
+        live = rho > 0.0
+        inv = np.divide(1.0, rho, out=np.zeros_like(rho), where=live)
         for a in range(3):
-            H[..., 0, idx[a]] += d[..., a] / rho
+            H[..., 0, idx[a]] += d[..., a] * inv
         H[..., 0, idx[3]] += 1.0
         return h, H
     if name == "multi_receiver_range_3d":

@@ -41,6 +41,20 @@ def test_host_side_entry_points_without_gpu():
     assert lib.mhe_workspace_bytes(d, 2) > 2 * 8 * (64 * 65 // 2) * 256
 
 
+def test_set_option_is_explicit_and_bounded():
+    """The A/B options are set only through mhe_set_option (no environment variable is
+    read): it returns the previous value and refuses unknown options / bad values."""
+    lib = _lib.load()
+    assert lib.mhe_set_option(_lib.OPT_BIG_RIGHT_LOOKING, 1) == 0
+    assert lib.mhe_set_option(_lib.OPT_BIG_RIGHT_LOOKING, 0) == 1
+    assert lib.mhe_set_option(_lib.OPT_DEBUG_SMEM_PAD, 0) == 0
+    assert lib.mhe_set_option(_lib.OPT_DEBUG_SMEM_PAD, -5) == -1
+    assert lib.mhe_set_option(77, 1) == -1
+    src = open(os.path.join(ROOT, "nlp-filter_amd", "csrc", "mhe_core.h")).read()
+    src += open(os.path.join(ROOT, "nlp-filter_amd", "csrc", "mhe_gn.hip")).read()
+    assert "getenv" not in src
+
+
 def test_general_problem_dims_validation():
     """Extra variables / equality constraints / mixed rows: host-side checks."""
     lib = _lib.load()

@@ -16,7 +16,7 @@ torch = pytest.importorskip("torch")
 
 pytestmark = pytest.mark.gpu
 
-from mhe import configs, solver  # noqa: E402
+from mhe import _lib, configs, solver  # noqa: E402
 from oracle import gn  # noqa: E402
 
 import tolerance as tl  # noqa: E402
@@ -145,9 +145,10 @@ def test_big_wide_slab_c4_shape_matches_oracle():
 
 
 @pytest.mark.parametrize("cfg", ["c3", "c4"])
-def test_left_and_right_looking_factorizations_agree(cfg, monkeypatch):
+def test_left_and_right_looking_factorizations_agree(cfg):
     """k_big_chol's left-looking block-column update (default) and the right-looking
-    trailing update (MHE_BIG_LL=0, kept for A/B runs) accumulate every tile's updates in
+    trailing update (mhe_set_option(MHE_OPT_BIG_RIGHT_LOOKING, 1), kept for A/B runs)
+    accumulate every tile's updates in
     the same k order (the right-looking form only stores and reloads the partial sums
     between super-blocks, which is exact): iterates after 2 GN steps are bitwise
     identical (C3 reduced N = 60 with the 4-wide instance, C4 full shape with the 8-wide
@@ -156,10 +157,13 @@ def test_left_and_right_looking_factorizations_agree(cfg, monkeypatch):
     s = solver.from_workload(w)
     assert s.large_system
     out = {}
-    for ll in ("1", "0"):
-        monkeypatch.setenv("MHE_BIG_LL", ll)
-        out[ll] = _np(s.solve(w.X_init, w.U, w.Y, w.PAR, max_iter=2, tol=0.0))
-        torch.cuda.synchronize()
+    try:
+        for ll in ("1", "0"):
+            assert s.lib.mhe_set_option(_lib.OPT_BIG_RIGHT_LOOKING, 0 if ll == "1" else 1) >= 0
+            out[ll] = _np(s.solve(w.X_init, w.U, w.Y, w.PAR, max_iter=2, tol=0.0))
+            torch.cuda.synchronize()
+    finally:
+        s.lib.mhe_set_option(_lib.OPT_BIG_RIGHT_LOOKING, 0)
     Xa, Xb = out["1"][0], out["0"][0]
     assert (out["1"][3] == out["0"][3]).all() and (out["1"][2] == out["0"][2]).all()
     print(f"{cfg}: left- vs right-looking max|dX| = {np.abs(Xa - Xb).max():.3e}")
