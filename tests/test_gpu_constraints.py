@@ -144,3 +144,23 @@ def test_bounds_with_equality_constraints_match_oracle():
     Xg = _check(problem, w, eq_rows, problem._ineq_rows())
     assert Xg[:, 1].max() <= ub + 1e-9
     assert np.abs(Xg[[0, 5, 9], 0] - Xg[[0, 5, 9], 1]).max() <= 1e-9 * (1 + np.abs(Xg).max())
+
+
+@pytest.mark.gpu
+def test_constants_stamp_covers_equality_rows():
+    """mhe_dims.eq_idx / eq_rhs are copied into the constants buffer at build time and
+    stamped into its layout tag: a caller that changes the rows in place and solves
+    without rebuilding gets MHE_STATUS_BAD_CONSTANTS, not the old rows."""
+    from mhe import solver
+    w = configs.make_c2(B=2, N=20)
+    s = solver.BatchSolver(w.N, w.T, w.dyn, w.meas, w.cpm.D, (w.T / 2) * w.cpm.w, w.cpm.lagrange_matrix(w.t_meas),
+                           w.Qw, w.Rw, eq=[[0, 2]], eq_rhs=[0.0])
+    X, cost, iters, status = s.solve(w.X_init, w.U, w.Y, max_iter=3, tol=0.0)
+    assert (status.cpu().numpy() != solver.STATUS_BAD_CONSTANTS).all()
+    s._eq_rhs[0] = 0.5        # dims.eq_rhs points at this array: the stale-row case
+    X, cost, iters, status = s.solve(w.X_init, w.U, w.Y, max_iter=3, tol=0.0)
+    assert (status.cpu().numpy() == solver.STATUS_BAD_CONSTANTS).all()
+    s._eq_rhs[0] = 0.0
+    s._eq[0] = 1              # other row indices, same count
+    X, cost, iters, status = s.solve(w.X_init, w.U, w.Y, max_iter=3, tol=0.0)
+    assert (status.cpu().numpy() == solver.STATUS_BAD_CONSTANTS).all()
