@@ -10,8 +10,9 @@ C2  van_der_pol:       n=2, m=1 (u = 0), full_state, N=100, T=10, M=101, B=1024
     (van_der_pol.py:10,33 scales; R, Q from estimation_example.py:20,33)
 C3  gnss_stationary:   n=5, m=3, pseudorange, N=200, T=200, 201 epochs x 12 sats, B=4096
     (large-system path: d = 1005)
-C4  rc-car:            kinematic_bycicle_and_bias (n=6, m=2) + pseudorange, N=500, T=500,
-    501 epochs x 12 sats, B=8192 over 8 GPUs (d = 3006; rc-car.py:46-47,89-113 at N=500)
+C4  rc-car:            kinematic_bycicle_and_bias (n=6, m=2) + pseudorange, N=500, T=100 s
+    of the reference's rc-car logs (px4 controls, 101 GNSS epochs x 12 slots), B=8192
+    over 8 GPUs (d = 3006; rc-car.py:21-47,89-113 at N=500)
 C5  multi-receiver:    multi_receiver (n=8, m=0) + pseudorange + pseudorange_rate per
     satellite and a 2-D range to the extra variable XA (n_extra=3) per epoch -- mixed
     rows, N=200, T=200, 201 epochs x (12 + 12 + 1) rows, B=16384 over 8 GPUs
@@ -205,43 +206,60 @@ def bicycle_rhs(x, u):
                      (v / L) * np.tan(delta)], axis=1)
 
 
-def make_c4(B=1024, seed=3, N=500, epochs=None, n_sat=12):
-    """C4 rc-car shape: bicycle + pseudorange, N=500 (d = 3006).  Synthetic controls
-    (throttle ~0.3, smooth steering) per trajectory, RK4 truth, r_pr and Q as
-    rc-car.py:46-47; 12 satellite slots fixed over the window."""
-    T = float(N)
-    epochs = N + 1 if epochs is None else epochs
+def rc_car_inputs():
+    """The reference's rc-car inputs (tests/golden/rc_car_c4.npz, written by
+    tests/golden/gen_golden.py gen_rc_car_c4 from data/rc-car/px4/log_164_*.ulg and
+    data/rc-car/gnss/gnss_log_2020_02_27_10_02_20*.mat exactly as px4/convert.py and
+    rc-car.py:21-38 process them): px4 times t_u (s, from 0) and controls u (2, T')
+    [throttle, steer]; GNSS epoch times t_gnss, ENU satellite positions sat_enu
+    (E, 12, 3), slot counts, pseudoranges."""
+    import os
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "tests", "golden", "rc_car_c4.npz")
+    return np.load(path)
+
+
+def make_c4(B=1024, seed=3, N=500, T=100.0):
+    """C4 rc-car: kinematic_bycicle_and_bias (n=6, m=2) + pseudorange,
+    N=500 (d = 3006), on the reference's own rc-car data over the first T = 100 s: the
+    throttle / steering of data/rc-car/px4/log_164 (250 Hz; setControl interpolates them
+    at the nodes, nlp/nlp.py:304-308) and the satellite epochs of
+    data/rc-car/gnss/gnss_log_2020_02_27_10_02_20 (101 epochs x 12 slots, 9-12 live:
+    empty slots R = 0, as the scripts mask them) -- rc_car_inputs().  Per trajectory:
+    a seeded initial state (position, heading, clock bias and drift), the truth
+    integrated from those controls (RK4, 25 sub-steps a second), pseudoranges at the
+    real satellite positions with r_pr = 10 (rc-car.py:47); Q as rc-car.py:46.  No
+    heading rows: rc-car.py:89-114 adds pseudoranges only."""
+    z = rc_car_inputs()
+    ep = np.nonzero(z["t_gnss"] <= T + 1e-9)[0]
+    t_ep, sat, cnt = z["t_gnss"][ep], z["sat_enu"][ep], z["count"][ep]
+    epochs, n_sat = t_ep.size, sat.shape[1]
+    live = np.arange(n_sat)[None, :] < cnt[:, None]
     rng = np.random.default_rng(seed)
-    t_ep = np.linspace(0, T, epochs)
-    sat = _sky(rng, n_sat)
-    ph = rng.uniform(0, 2 * np.pi, (B, 2))
-    th0 = rng.uniform(0.25, 0.35, (B, 1))
+    uf = interp1d(z["t_u"], z["u"], fill_value="extrapolate")
 
     def ctrl(t):
-        t = np.atleast_1d(t)
-        return np.stack([th0 + 0.03 * np.sin(2 * np.pi * t[None, :] / 47.0 + ph[:, :1]),
-                         0.4 * np.sin(2 * np.pi * t[None, :] / 61.0 + ph[:, 1:])], axis=-1)  # (B, len t, 2)
+        return np.broadcast_to(uf(np.atleast_1d(t)).T[None], (B, np.size(t), 2))
 
     x0 = np.zeros((B, 6))
     x0[:, :2] = rng.normal(size=(B, 2)) * 10.0
     x0[:, 2] = rng.uniform(-np.pi, np.pi, B)
     x0[:, 3] = rng.normal(size=B) * 100.0
     x0[:, 4] = rng.normal(size=B) * 0.5
-    xt = _rk4(lambda tt, x: bicycle_rhs(x, ctrl(tt)[:, 0]), x0, t_ep, substeps=4)
+    xt = _rk4(lambda tt, x: bicycle_rhs(x, ctrl(tt)[:, 0]), x0, t_ep, substeps=25)
     r_pr = 10.0
-    rho = np.linalg.norm(xt[:, :, None, :3] - sat[None, None], axis=-1) + xt[:, :, None, 3]
+    rho = np.linalg.norm(xt[:, :, None, :3] - sat[None], axis=-1) + xt[:, :, None, 3]
     M = epochs * n_sat
-    Y = (rho + rng.normal(size=rho.shape) * np.sqrt(r_pr)).reshape(B, M, 1)
+    Y = np.where(live[None], rho + rng.normal(size=rho.shape) * np.sqrt(r_pr), 0.0).reshape(B, M, 1)
     cpm = ChebyshevPseudospectralMethod(N, 0, T)
     t_nodes = cpm.tau2t(cpm.tau)
-    U = ctrl(t_nodes)
+    U = interp1d(z["t_u"], z["u"], fill_value="extrapolate")(t_nodes).T[None]   # setControl
     X_init = interp1d(t_ep, xt, axis=1)(t_nodes) + rng.normal(size=(B, 1, 6)) * np.array([2.0, 2.0, 0.02, 2.0, 0.05, 0.1])
     Q = np.diag([1, 1, 0.001, .01, .01, 1])
+    Rw = np.where(live.reshape(-1), 1.0 / r_pr, 0.0)[:, None, None]
     return Workload(name="C4_rc_car", N=N, T=T, n=6, m=2, p=1, M=M, B=B,
                     dyn="kinematic_bycicle_and_bias", meas="pseudorange", meas_static={"idx": [0, 1, 2, 3]},
-                    t_meas=np.repeat(t_ep, n_sat), Y=Y, U=U, PAR=np.tile(sat, (epochs, 1))[None],
-                    Qw=np.linalg.inv(Q), Rw=np.full((M, 1, 1), 1.0 / r_pr), Pw=None, x0=None,
-                    X_init=X_init, X_true=xt, cpm=cpm)
+                    t_meas=np.repeat(t_ep, n_sat), Y=Y, U=U, PAR=sat.reshape(1, M, 3),
+                    Qw=np.linalg.inv(Q), Rw=Rw, Pw=None, x0=None, X_init=X_init, X_true=xt, cpm=cpm)
 
 
 def pr_row(idx, sat):

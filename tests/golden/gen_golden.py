@@ -517,11 +517,115 @@ def gen_autocar_ekf(ref):
                         plug_y=np.stack(py), plug_H=np.stack(pH))
 
 
+def read_ulog(path, topics):
+    """Minimal ULog reader (the documented PX4 binary log format; nothing in the file is
+    executed): the 16-byte header, then messages [uint16 size][uint8 type][body].
+    'F' bodies are "name:type field;type field;...", 'A' bodies subscribe a topic
+    (uint8 multi_id, uint16 msg_id, name), 'D' bodies are uint16 msg_id + the fields
+    packed in format order.  Returns {topic: {field: array}} for multi_id 0 of `topics`,
+    with the columns ulog2csv would write (padding dropped, arrays flattened as
+    field[i], timestamp first)."""
+    import struct
+    raw = open(path, "rb").read()
+    assert raw[:7] == b"ULog\x01\x125", "not a ULog file"
+    sizes = {"int8_t": 1, "uint8_t": 1, "bool": 1, "char": 1, "int16_t": 2, "uint16_t": 2, "int32_t": 4,
+             "uint32_t": 4, "float": 4, "int64_t": 8, "uint64_t": 8, "double": 8}
+    codes = {"int8_t": "b", "uint8_t": "B", "bool": "?", "char": "c", "int16_t": "h", "uint16_t": "H",
+             "int32_t": "i", "uint32_t": "I", "float": "f", "int64_t": "q", "uint64_t": "Q", "double": "d"}
+    formats, subs, rows = {}, {}, {}
+    off = 16
+    while off + 3 <= len(raw):
+        size, typ = struct.unpack_from("<HB", raw, off)
+        body = raw[off + 3: off + 3 + size]
+        off += 3 + size
+        if len(body) < size:
+            break
+        if typ == ord("F"):
+            name, spec = body.decode("ascii").split(":", 1)
+            fields = []
+            for item in spec.strip(";").split(";"):
+                ftype, fname = item.split(" ")
+                count = 1
+                if "[" in ftype:
+                    ftype, cnt = ftype[:-1].split("[")
+                    count = int(cnt)
+                fields.append((ftype, fname, count))
+            formats[name] = fields
+        elif typ == ord("A"):
+            multi, msg_id = struct.unpack_from("<BH", body, 0)
+            name = body[3:].decode("ascii")
+            if name in topics and multi == 0:
+                subs[msg_id] = name
+                rows[name] = []
+        elif typ == ord("D"):
+            (msg_id,) = struct.unpack_from("<H", body, 0)
+            if msg_id in subs:
+                rows[subs[msg_id]].append(body[2:])
+    out = {}
+    for name in topics:
+        fields = formats[name]
+        fmt = "<" + "".join(codes[t] * c if c > 1 else codes[t] for t, _, c in fields)
+        cols = []
+        for t, fn, c in fields:
+            cols += [f"{fn}[{i}]" for i in range(c)] if c > 1 else [fn]
+        keep = [i for i, cn in enumerate(cols) if not cn.startswith("_padding")]
+        full = struct.calcsize(fmt)   # PX4 does not log a message's trailing padding: pad it back
+        vals = np.array([struct.unpack_from(fmt, r + bytes(full - len(r)), 0) for r in rows[name]], dtype=np.float64)
+        names = [cols[i] for i in keep]
+        order = [names.index("timestamp")] + [i for i, cn in enumerate(names) if cn != "timestamp"]
+        out[name] = {"columns": [names[i] for i in order], "data": vals[:, keep][:, order]}
+    return out
+
+
+def gen_rc_car_c4(ref):
+    """C4 inputs from the reference's rc-car logs (rc-car.py:21-38):
+    * controls: data/rc-car/px4/log_164_*.ulg read with read_ulog and processed exactly
+      as px4/convert.py (ulog2csv columns manual_control_setpoint[3], [4] = throttle,
+      steer; sensor_combined timestamps; microseconds -> s, zeroed at the earlier first
+      sample; the control interp1d'd onto the sensor times) and rc-car.py:25-37
+      (throttle < 0.1 -> 0; start at the first |steer| < 0.01; times from 0).  The .pkl
+      next to it (convert.py's output) is a pickle and is not read.
+    * satellites: data/rc-car/gnss/gnss_log_2020_02_27_10_02_20 through the reference's
+      load_gnss_logs, rotated to ENU at the scripts' reference point by its ecef2enu,
+      times from 0 (rc-car.py:35); up to 12 slots per epoch (count)."""
+    from scipy.interpolate import interp1d
+    u = read_ulog(f"{REF}/data/rc-car/px4/log_164_2020-2-27-10-03-56.ulg", ("manual_control_setpoint", "sensor_combined"))
+    mc, sc = u["manual_control_setpoint"]["data"], u["sensor_combined"]["data"]
+    t1, throttle, steer = mc[:, 0] * 1e-6, mc[:, 3], mc[:, 4]
+    t2 = sc[:, 0] * 1e-6
+    t0 = np.min([t1[0], t2[0]])
+    t1 = t1 - t0
+    t2 = t2 - t0
+    control = interp1d(t1, np.vstack((throttle, steer)), fill_value="extrapolate")(t2)
+    for i in range(control.shape[1]):          # rc-car.py:25-28
+        if control[0, i] < 0.1:
+            control[0, i] = 0.0
+    for k, t in enumerate(t2):                # rc-car.py:30-35
+        if np.abs(control[1, k]) < 0.01:
+            t2, control = t2[k:], control[:, k:]
+            break
+    t2 = t2 - t2[0]
+    g = ref.data.load_gnss_logs(f"{REF}/data/rc-car/gnss/gnss_log_2020_02_27_10_02_20")
+    tg = np.asarray(list(g["t"]), dtype=np.float64)
+    tg = tg - tg[0]
+    p_ref = ref.gutils.lla2ecef(np.array([37.4276, -122.1670, 0.0]))
+    E, S = len(g["sat_pos"]), 12
+    sat, cnt, pr = np.zeros((E, S, 3)), np.zeros(E, dtype=np.int32), np.zeros((E, S))
+    for k in range(E):
+        sp = g["sat_pos"][k]
+        cnt[k] = sp.shape[0]
+        for j in range(cnt[k]):
+            sat[k, j] = ref.gutils.ecef2enu(sp[j, :], p_ref)
+            pr[k, j] = g["pr"][k][j]
+    np.savez_compressed(os.path.join(OUT, "rc_car_c4.npz"), t_u=t2, u=control, t_gnss=tg, sat_enu=sat, count=cnt,
+                        pr=pr, ulog_columns=np.array(u["manual_control_setpoint"]["columns"][:5]))
+
+
 def main(which=None):
     ref = load_reference()
     gens = {"collocation": gen_collocation, "plugins": gen_plugins, "ekf": gen_ekf, "gnss_io": gen_gnss_io,
             "least_squares": gen_least_squares, "c3_geometry": gen_c3_geometry,
-            "autocar_ekf": gen_autocar_ekf}
+            "autocar_ekf": gen_autocar_ekf, "rc_car_c4": gen_rc_car_c4}
     for name, fn in gens.items():
         if not which or name in which:
             fn(ref)

@@ -44,7 +44,8 @@ def test_c4_full_shape_matches_oracle():
     pb = gn.Problem(w.N, w.T, w.n, w.m, w.dyn, w.meas, w.cpm.D, (w.T / 2) * w.cpm.w,
                     w.cpm.lagrange_matrix(w.t_meas), w.Qw, w.Rw, meas_static=w.meas_static)
     PAR = np.broadcast_to(w.PAR, (w.B,) + w.PAR.shape[1:])
-    run = lambda Y, pt=None: gn.gauss_newton(pb, w.X_init, w.U, Y, PAR, max_iter=2, tol=0.0, perturb=pt)  # noqa: E731
+    U = np.broadcast_to(w.U, (w.B,) + w.U.shape[1:])   # the rc-car controls, shared by the batch
+    run = lambda Y, pt=None: gn.gauss_newton(pb, w.X_init, U, Y, PAR, max_iter=2, tol=0.0, perturb=pt)  # noqa: E731
     Xr, cr, ir, sr = run(w.Y)
     fx, fc = tl.floor(lambda Y, pt: run(Y, pt)[:2], w.Y)
     assert iters.tolist() == ir.tolist() == [2, 2] and status.tolist() == sr.tolist()
@@ -179,3 +180,44 @@ def test_chunks_are_whole_cu_fulls():
         assert s._chunk(3) == 3
     finally:
         s.ws_budget = None
+
+
+def _subset_vs_oracle(w, X, cost, iters, status, idx, its, what):
+    """Strided trajectories of a configured-size batch vs the oracle on those inputs
+    (catches batch-index and workspace-offset bugs that a B = 2 run cannot)."""
+    pb = gn.Problem(w.N, w.T, w.n, w.m, w.dyn, w.meas, w.cpm.D, (w.T / 2) * w.cpm.w,
+                    w.cpm.lagrange_matrix(w.t_meas), w.Qw, w.Rw, meas_static=w.meas_static)
+    U = np.broadcast_to(w.U, (w.B,) + w.U.shape[1:])[idx] if w.U.shape[0] == 1 else w.U[idx]
+    PAR = np.broadcast_to(w.PAR, (idx.size,) + w.PAR.shape[1:])
+    run = lambda Y, pt=None: gn.gauss_newton(pb, w.X_init[idx], U, Y, PAR, max_iter=its, tol=0.0,  # noqa: E731
+                                             perturb=pt)
+    Xr, cr, ir, sr = run(w.Y[idx])
+    fx, fc = tl.floor(lambda Y, pt: run(Y, pt)[:2], w.Y[idx])
+    assert iters[idx].tolist() == ir.tolist() == [its] * idx.size and status[idx].tolist() == sr.tolist()
+    assert iters.tolist() == [its] * w.B and status.tolist() == [status[0]] * w.B
+    b = tl.bound(fx, Xr)
+    tl.check(f"{what} X (trajectories {idx.tolist()})", np.abs(X[idx] - Xr).max(), b, " m")
+    tl.check(f"{what} cost", np.abs(cost[idx] - cr).max(), tl.FLOOR_MULT * fc + 1e-10 * np.abs(cr).max())
+    return b
+
+
+def test_c3_configured_batch_strided_subset_matches_oracle():
+    """C3 at its configured batch (B = 4096, real geometry), 2 GN iterations on the
+    device; 8 trajectories spread over the batch (first, last, strided) vs the oracle."""
+    w = configs.make_c3(B=4096)
+    s = solver.from_workload(w)
+    X, cost, iters, status = _np(s.solve(w.X_init, w.U, w.Y, w.PAR, max_iter=2, tol=0.0))
+    idx = np.unique(np.r_[np.arange(0, w.B, w.B // 7), w.B - 1])[:8]
+    assert _subset_vs_oracle(w, X, cost, iters, status, idx, 2, "C3 B=4096") < 1e-4
+
+
+def test_c4_configured_batch_strided_subset_matches_oracle():
+    """C4 at its configured per-GPU batch (B = 1024, d = 3006), 2 GN iterations (the
+    batch chunked through one workspace if the free HBM asks for it); 3 strided
+    trajectories vs the oracle under C4's conditioning-limited bound (~1 cm)."""
+    w = configs.make_c4(B=1024)
+    s = solver.from_workload(w)
+    print("C4 B=1024 chunk", s._chunk(w.B))
+    X, cost, iters, status = _np(s.solve(w.X_init, w.U, w.Y, w.PAR, max_iter=2, tol=0.0))
+    idx = np.array([0, 511, 1023])
+    _subset_vs_oracle(w, X, cost, iters, status, idx, 2, "C4 B=1024")
