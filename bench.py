@@ -244,6 +244,11 @@ def main():
                 rec["roofline"]["traffic"] = ps["hbm_bytes_per_launch"]
                 rec["roofline"]["traffic_note"] = ps["note"] + f"; profiled build {ps['lib_sha']} ({ps['tag']})"
                 rec["roofline"]["mfma_util_pmc"] = ps.get("mfma_util")
+                if ps.get("trace_ms_timed_launches"):
+                    # the same quantity as kernel_ms from the rocprof trace of that build: the
+                    # average over the profiled bench's timed launches (its warm-up excluded)
+                    rec["roofline"]["kernel_ms_rocprof_timed"] = ps["trace_ms_timed_launches"]
+                    rec["roofline"]["kernel_ms_rocprof_all"] = ps["trace_ms_all_launches"]
             elif same:
                 rec["roofline"]["traffic_note"] = (f"profiles/pmc_summary.json measured build {ps.get('lib_sha')}, "
                                                    f"not this libmhe.so ({lib_digest()}): traffic omitted")

@@ -77,7 +77,7 @@ __host__ __device__ inline BigWs big_ws_layout(int P, int M, int n, int NT, int 
   W.XE = o;  o = al(o + (size_t)Mr * n);
   W.GEe = o; o = al(o + (size_t)Mr * n);
   W.Ge = o;  o = al(o + (size_t)Mr * n * n);
-  W.Es = o;  o = al(o + (size_t)P * n * n);
+  W.Es = o;  o = al(o + (size_t)P * n * n);  // E_k = c_k Qw F_k, component-major [(a n + b) P + k]
   W.FtE = o; o = al(o + (size_t)P * n * n);
   W.Vs = o;  o = al(o + (size_t)P * n);
   W.FtV = o; o = al(o + (size_t)P * n);
@@ -231,12 +231,13 @@ __device__ void big_nodes_sparse(const BigArgs& a, const BigConst& CL, const Big
     DYN::eval_sparse(X + k * n, uk, a.dpar, f, Fv);
     for (int c = 0; c < n; ++c) W[c] = a.alpha * W[c] - f[c];
     const double ck = cw[k];
-    double* Ek = ws + WL.Es + (size_t)k * n * n;
+    double* Ek = ws + WL.Es + k;  // component-major: E_k[r][c] at (r n + c) P + k
     double* Vk = ws + WL.Vs + (size_t)k * n;
     double* FtV = ws + WL.FtV + (size_t)k * n;
     double* FtE = ws + WL.FtE + (size_t)k * n * n;
+    const size_t P_ = a.P;
     for (int c = 0; c < n * n; ++c) {
-      Ek[c] = 0.0;
+      Ek[c * P_] = 0.0;
       FtE[c] = 0.0;
     }
     for (int r = 0; r < n; ++r) {
@@ -249,13 +250,13 @@ __device__ void big_nodes_sparse(const BigArgs& a, const BigConst& CL, const Big
         cost += ck * (2.0 * q * dl * dl * (sr - 1.0));
         ws[WL.LAM + k * n + r] = lam;
         for (int z = 0; z < NNZ; ++z)
-          if (DYN::frow(z) == r) Ek[r * n + DYN::fcol(z)] = lam * Fv[z];
+          if (DYN::frow(z) == r) Ek[(r * n + DYN::fcol(z)) * P_] = lam * Fv[z];
       } else {
         double s = 0.0;
         for (int c = 0; c < n; ++c) s += Qw[r * n + c] * W[c];
         v = ck * s;
         cost += W[r] * v;
-        for (int z = 0; z < NNZ; ++z) Ek[r * n + DYN::fcol(z)] += ck * Qw[r * n + DYN::frow(z)] * Fv[z];
+        for (int z = 0; z < NNZ; ++z) Ek[(r * n + DYN::fcol(z)) * P_] += ck * Qw[r * n + DYN::frow(z)] * Fv[z];
       }
       Vk[r] = v;
       FtV[r] = 0.0;
@@ -263,7 +264,7 @@ __device__ void big_nodes_sparse(const BigArgs& a, const BigConst& CL, const Big
     for (int z = 0; z < NNZ; ++z) {
       const int t = DYN::frow(z), r = DYN::fcol(z);
       FtV[r] += Fv[z] * Vk[t];
-      for (int c = 0; c < n; ++c) FtE[r * n + c] += Fv[z] * Ek[t * n + c];
+      for (int c = 0; c < n; ++c) FtE[r * n + c] += Fv[z] * Ek[(t * n + c) * P_];
     }
   }
 }
@@ -321,7 +322,8 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_resid(BigArgs a, int final
     double W[n], V[n];
     for (int c = 0; c < n; ++c) W[c] = a.alpha * dx[c] - f[c];
     const double ck = cw[k];
-    double* Ek = ws + WL.Es + (size_t)k * n * n;
+    double* Ek = ws + WL.Es + k;  // component-major: E_k[r][c] at (r n + c) P + k
+    const size_t P_ = a.P;
     if (a.huber) {
       // pseudo_huber_loss (cost_functions.py:25-31) by IRLS, as k_gn: lambda = c q / sqrt(1 +
       // W^2 / delta^2) per component (only diag(Qw) enters), V = lambda W, E = diag(lambda) F
@@ -333,7 +335,7 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_resid(BigArgs a, int final
         V[r] = lam * W[r];
         cost += ck * (2.0 * q * dl * dl * (sr - 1.0));
         ws[WL.LAM + k * n + r] = lam;
-        for (int c = 0; c < n; ++c) Ek[r * n + c] = lam * F[r * n + c];
+        for (int c = 0; c < n; ++c) Ek[(r * n + c) * P_] = lam * F[r * n + c];
       }
     } else {
       for (int r = 0; r < n; ++r) {
@@ -344,7 +346,7 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_resid(BigArgs a, int final
         for (int c = 0; c < n; ++c) {
           double e = 0.0;
           for (int t = 0; t < n; ++t) e += Qw[r * n + t] * F[t * n + c];
-          Ek[r * n + c] = ck * e;
+          Ek[(r * n + c) * P_] = ck * e;
         }
       }
     }
@@ -358,7 +360,7 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_resid(BigArgs a, int final
     for (int r = 0; r < n; ++r)
       for (int c = 0; c < n; ++c) {
         double u = 0.0;
-        for (int t = 0; t < n; ++t) u += F[t * n + r] * Ek[t * n + c];
+        for (int t = 0; t < n; ++t) u += F[t * n + r] * Ek[(t * n + c) * P_];
         ws[WL.FtE + (k * n + r) * n + c] = u;
       }
   }
@@ -572,6 +574,21 @@ inline void big_pair_plan(BigArgs& A, unsigned long long support) {  // bit c: c
   A.nch = A.nchl + (A.npr - nl + BIG_PCH - 1) / BIG_PCH;
 }
 
+// Epoch-GEMM staging of k_big_assemble: BIG_AKC epochs per chunk, double-buffered in LDS --
+// the two 16-row Phi_E column blocks of the tile position and G_e[pair] of every pair the
+// workgroup's waves contract (WPB waves x BIG_PCH pairs)
+constexpr int BIG_AKC = 32;
+__host__ __device__ constexpr int big_asm_lds(int wpb) { return 2 * (2 * BIG_AKC * 16 + wpb * BIG_PCH * BIG_AKC); }  // doubles
+
+// Work items are (tile position (it, jt), pair chunk), one wave each. The chunks with
+// measurement-coupled ("live") pairs come first: a workgroup of WPB waves takes one
+// position and WPB live chunks, so the waves share the position's Phi_E rows -- per chunk
+// of BIG_AKC epochs the workgroup stages Phi_E[e][16 it + r], Phi_E[e][16 jt + r] and its
+// pairs' G_e into LDS with global loads issued one chunk ahead (their latency hides under
+// the current chunk's MFMAs), and each wave's K steps read their operands from LDS (round
+// 3: every wave streamed its own operands from L2/HBM, two K steps ahead -- MFMA busy
+// ~25 %). The remaining blocks take the chunks without an epoch GEMM, WPB consecutive
+// (position, chunk) items per workgroup, no barriers.
 template <class DYN, class MEAS>
 __global__ __launch_bounds__(256, 4) void k_big_assemble(BigArgs a) {
   constexpr int n = DYN::n, p = MEAS::p;
@@ -587,78 +604,121 @@ __global__ __launch_bounds__(256, 4) void k_big_assemble(BigArgs a) {
   const double* Pw = (const double*)(a.cbuf + CL.Pw);
   const double* PhiE = (const double*)(a.cbuf + CL.PhiE);
   const int E = a.M > 0 ? *(const int*)(a.cbuf + CL.ne) : 0;
-  const int E4 = (E + 3) & ~3;  // K steps of 4 epochs (av = bv = 0 past E)
   // wave-uniform work decomposition (SGPRs: the tile position, pair chunk and table reads are scalar)
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int WPB = blockDim.x >> 6, nthr = blockDim.x;
   const int NTc = a.NTc, P = a.P, NCH = a.nch;
   const int npos = NTc * (NTc + 1) / 2;
-  const int u = blockIdx.x * 4 + wave;
-  if (u >= npos * NCH) return;
-  const int ch = u % NCH;
-  int it = 0, pos = u / NCH;  // pos -> (it, jt), jt <= it
+  const int nlg = (a.nchl + WPB - 1) / WPB;  // live groups per position
+  const bool gblock = (int)blockIdx.x < npos * nlg;
+  int grp = 0, pos, ch;
+  if (gblock) {
+    grp = blockIdx.x % nlg;
+    pos = blockIdx.x / nlg;
+    ch = grp * WPB + wave;
+  } else {
+    const int nd = NCH - a.nchl, item = ((int)blockIdx.x - npos * nlg) * WPB + wave;
+    pos = item / nd;
+    ch = a.nchl + item % nd;
+    if (pos >= npos) return;  // tail of the last block (no barriers on this side)
+  }
+  int it = 0;  // pos -> (it, jt), jt <= it
   while (pos > it) {
     pos -= it + 1;
     ++it;
   }
   const int jt = pos;
+  const bool valid = ch < NCH && (!gblock || ch < a.nchl);
   // this wave's pairs: table entries [q0, q0 + np) (BigPairPlan)
-  const bool live = ch < a.nchl;
-  const int q0 = live ? ch * a.pchl : a.nlive + (ch - a.nchl) * BIG_PCH;
-  const int np = min(live ? a.pchl : BIG_PCH, (live ? a.nlive : a.npr) - q0);
+  const bool live = valid && ch < a.nchl;
+  const int q0 = !valid ? 0 : live ? ch * a.pchl : a.nlive + (ch - a.nchl) * BIG_PCH;
+  const int np = !valid ? 0 : min(live ? a.pchl : BIG_PCH, (live ? a.nlive : a.npr) - q0);
   d4 acc[BIG_PCH];
 #pragma unroll
   for (int q = 0; q < BIG_PCH; ++q) acc[q] = d4{0.0, 0.0, 0.0, 0.0};
-  const int row = 16 * it + (lane & 15), col = 16 * jt + (lane & 15);
-  const bool vr = row < P, vc = col < P;
   const double* Ge = ws + WL.Ge;
-  if (live) {
-    int goff[BIG_PCH];  // offsets of G_e[ca][cb] for the chunk's pairs
-#pragma unroll
-    for (int q = 0; q < BIG_PCH; ++q) goff[q] = q < np ? a.pa[q0 + q] * n + a.pb[q0 + q] : 0;
-    // K steps of 4 epochs, software-pipelined: step e0 + 4's Phi_E and G_e loads are
-    // issued before step e0's MFMAs.  Raw buffer loads over exactly the E epochs: a lane
-    // past the last epoch (or on a padding row / column of the last tile) reads out of
-    // range and gets 0 from the hardware bounds check -- no clamps or selects, and the
-    // whole address is one 32-bit VGPR offset advanced by a constant per step.
+  if (gblock && E > 0) {  // workgroup-uniform
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    constexpr int KC = BIG_AKC, SA = KC * 16, SGW = BIG_PCH * KC;
+    const int SBUF = 2 * SA + WPB * SGW;
+    // staging sources: raw buffer loads with the hardware bounds check -- a slot past the
+    // last epoch, on a padding row / column, or of an absent pair reads 0
     const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc((void*)PhiE, (short)0, E * P * 8, 0x00020000);
     const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc((void*)Ge, (short)0, E * n * n * 8, 0x00020000);
     constexpr int OOB = 0x40000000;
-    const int eg = lane >> 4;
-    int oa = vr ? (eg * P + row) * 8 : OOB, ob = vc ? (eg * P + col) * 8 : OOB, og = eg * n * n * 8;
-    int gs[BIG_PCH];  // byte offsets of G_e[ca][cb] in an epoch's block (wave-uniform)
+    // Phi_E rows: shared by the workgroup, element idx = t + nthr k of [2][KC][16];
+    // G_e: private to the wave, element g = lane + 64 k of [BIG_PCH][KC]
+    constexpr int NAB = 2 * SA / 64, NG = (SGW + 63) / 64;
+    int gsrc[NG];  // pair offset within one epoch's G_e, or OOB
 #pragma unroll
-    for (int q = 0; q < BIG_PCH; ++q) gs[q] = 8 * goff[q];
-    const int da = 4 * P * 8, dg = 4 * n * n * 8;
-    // two K steps in flight (loads for e0 + 4 and e0 + 8 issued before step e0's MFMAs)
-    double av1, bv1, gv1[BIG_PCH], av2, bv2, gv2[BIG_PCH];
-    auto issue = [&](double& av, double& bv, double (&gv)[BIG_PCH]) {
-      av = bload(rp, oa, 0);
-      bv = bload(rp, ob, 0);
+    for (int k = 0; k < NG; ++k) {
+      const int g = lane + 64 * k, q = g / KC;
+      gsrc[k] = (g < SGW && q < np && live) ? (a.pa[q0 + q] * n + a.pb[q0 + q]) * 8 : OOB;
+    }
+    const int nchk = (E + KC - 1) / KC;
+    double sab[NAB], sg[NG];
+    auto fetch = [&](int c) {
 #pragma unroll
-      for (int q = 0; q < BIG_PCH; ++q) gv[q] = bload(rg, og + gs[q], 0);
-      oa += da;
-      ob += da;
-      og += dg;
-    };
-    issue(av1, bv1, gv1);
-    issue(av2, bv2, gv2);
-#pragma unroll 1
-    for (int e0 = 0; e0 < E4; e0 += 4) {
-      const double a0 = av1, b0 = bv1;
-      double g0[BIG_PCH];
-#pragma unroll
-      for (int q = 0; q < BIG_PCH; ++q) {
-        g0[q] = gv1[q];
-        gv1[q] = gv2[q];
+      for (int k = 0; k < NAB; ++k) {
+        const int idx = threadIdx.x + nthr * k;
+        if (idx < 2 * SA) {
+          const int rem = idx & (SA - 1), rowc = 16 * (idx >= SA ? jt : it) + (rem & 15);
+          sab[k] = bload(rp, rowc < P ? ((c * KC + (rem >> 4)) * P + rowc) * 8 : OOB, 0);
+        }
       }
-      av1 = av2;
-      bv1 = bv2;
-      issue(av2, bv2, gv2);  // the last two read past E: zeros, unused
 #pragma unroll
-      for (int q = 0; q < BIG_PCH; ++q)
-        if (q < np) acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0 * g0[q], b0, acc[q], 0, 0, 0);
+      for (int k = 0; k < NG; ++k) {
+        const int e = c * KC + (lane + 64 * k) % KC;
+        sg[k] = bload(rg, gsrc[k] >= OOB ? OOB : e * n * n * 8 + gsrc[k], 0);
+      }
+    };
+    auto deposit = [&](int buf) {
+      double* s0 = sm + buf * SBUF;
+#pragma unroll
+      for (int k = 0; k < NAB; ++k) {
+        const int idx = threadIdx.x + nthr * k;
+        if (idx < 2 * SA) s0[idx] = sab[k];
+      }
+#pragma unroll
+      for (int k = 0; k < NG; ++k) {
+        const int g = lane + 64 * k;
+        if (g < SGW) s0[2 * SA + wave * SGW + g] = sg[k];
+      }
+    };
+    fetch(0);
+    deposit(0);
+    __syncthreads();
+    const int eg = lane >> 4, r16 = lane & 15;
+#pragma unroll 1
+    for (int c = 0; c < nchk; ++c) {
+      const int buf = c & 1;
+      if (c + 1 < nchk) fetch(c + 1);  // in flight during this chunk's MFMAs
+      if (live) {
+        const double* sA = sm + buf * SBUF;
+        const double* sB = sA + SA;
+        const double* sG = sA + 2 * SA + wave * SGW;
+        // two K steps per trip (the MFMAs are convergent: no remainder loop); a step past
+        // the last epoch reads the zeros staged for it
+        const int ks = min(KC, E - c * KC);
+#pragma unroll 1
+        for (int e0 = 0; e0 < ks; e0 += 8) {
+#pragma unroll
+          for (int h = 0; h < 8; h += 4) {
+            const int e = e0 + h + eg;
+            const double a0 = sA[e * 16 + r16], b0 = sB[e * 16 + r16];
+#pragma unroll
+            for (int q = 0; q < BIG_PCH; ++q)
+              if (q < np) acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0 * sG[q * KC + e], b0, acc[q], 0, 0, 0);
+          }
+        }
+      }
+      if (c + 1 < nchk) deposit(buf ^ 1);
+      __syncthreads();
     }
   }
+  if (!valid) return;
+  const int row = 16 * it + (lane & 15), col = 16 * jt + (lane & 15);
+  const bool vr = row < P, vc = col < P;
   if (a.huber) {
     // pseudo-Huber IRLS: the dynamics part a^2 (D^T C D) (x) Qw is no longer constant --
     // block (ca, ca) gets a^2 D^T diag(c lambda_ca) D (k_big_resid's weights), a GEMM
@@ -692,7 +752,8 @@ __global__ __launch_bounds__(256, 4) void k_big_assemble(BigArgs a) {
       const int ca = a.pa[q0 + q], cb = a.pb[q0 + q];
       const double qab = a.huber ? 0.0 : a.alpha * a.alpha * Qw[ca * n + cb];
       const double pw = a.has_prior ? Pw[ca * n + cb] : 0.0;
-      const int sE1 = (int)(WL.Es * 8) + (ca * n + cb) * 8, sE2 = (int)(WL.Es * 8) + (cb * n + ca) * 8;
+      // E_l[ca][cb] and E_j[cb][ca] (component-major: node index fastest)
+      const int sE1 = (int)((WL.Es + (size_t)(ca * n + cb) * P) * 8), sE2 = (int)((WL.Es + (size_t)(cb * n + ca) * P) * 8);
       const int sF = (int)(WL.FtE * 8) + (ca * n + cb) * 8;
       // tile (it, jt) of block (ca, cb) and, off the diagonal pair, its transpose into (jt, it)
 #pragma unroll
@@ -708,9 +769,14 @@ __global__ __launch_bounds__(256, 4) void k_big_assemble(BigArgs a) {
           const int j = 16 * ti + tr, l = 16 * tj + tc;
           double v;
           if (j < P && l < P) {
-            v = acc[q][r] + qab * bload(rc, (j * P + l) * 8, (int)CL.DCD) -
-                a.alpha * (bload(rc, (l * P + j) * 8, (int)CL.D) * bload(rw, l * n * n * 8, sE1) +
-                           bload(rc, (j * P + l) * 8, (int)CL.D) * bload(rw, j * n * n * 8, sE2));
+            // every operand read along the lane-varying index (l for the tile, j for its
+            // transpose): D_lj from D^T or D, D_jl from D or D^T, the exactly symmetric
+            // D^T C D either way, E component-major -- coalesced, not P- or n^2-strided
+            const int jl = (j * P + l) * 8, lj = (l * P + j) * 8;
+            const double dcd = bload(rc, tp ? lj : jl, (int)CL.DCD);
+            const double d_lj = tp ? bload(rc, lj, (int)CL.D) : bload(rc, jl, (int)CL.Dt);
+            const double d_jl = tp ? bload(rc, lj, (int)CL.Dt) : bload(rc, jl, (int)CL.D);
+            v = acc[q][r] + qab * dcd - a.alpha * (d_lj * bload(rw, l * 8, sE1) + d_jl * bload(rw, j * 8, sE2));
             if (j == l) v += bload(rw, j * n * n * 8, sF);
             if (j == 0 && l == 0) v += pw;
           } else {
@@ -761,7 +827,9 @@ constexpr int BIG_WIDE_NT = MHE_BIG_WIDE_NT;
 #endif
 #ifndef MHE_BIG_KO
 #define MHE_BIG_KO 0  // knock-out mask for timing probes only (tools/ko_big.sh): 1 trailing / left-looking
-                      // update, 2 in-block, 4 TRSM, 8 the left-looking update's slab staging
+                      // update, 2 in-block, 4 TRSM, 8 the left-looking update's slab staging,
+                      // 16 the rows below the diagonal block, 32 the backward solve; any
+                      // nonzero mask also freezes X (k_big_update), 64 only that (the baseline)
 #endif
 constexpr int BIG_LB_TILES = BIG_KB * (BIG_KB - 1) / 2;
 // the LJ region: the trailing slab, or (panel phase) the in-block L tiles LB and the
@@ -943,7 +1011,7 @@ __global__ __launch_bounds__(BIG_NTHREADS, BIG_JB == 8 ? 2 : 4) void k_big_chol(
         for (int r = 0; r < 4; ++r) DT[64 * r + lane] = c[r];
         wave_lds_sync();
         const bool bad = panel(DT, UN, lane);
-        if (bad && lane == 0) *flag = 1;
+        if (bad && lane == 0 && !MHE_BIG_KO) *flag = 1;  // probes keep every trajectory running
         wave_lds_sync();
         block_fwd(DT, BV + 16 * k, YV + 16 * k, lane);  // y_k = L_kk^-1 b_k
         for (int e = lane; e < DTS; e += 64) {
@@ -1009,7 +1077,7 @@ __global__ __launch_bounds__(BIG_NTHREADS, BIG_JB == 8 ? 2 : 4) void k_big_chol(
     // +2 %, C5 +0.7 %); the 4-wide one keeps one row per wave (the second row's registers
     // spill there: C3 -0.9 %).  Unused second-row work is dead code at JB = 4.
     constexpr int RPW = BIG_JB == 8 ? 2 : 1;
-    for (int I = kend + wave; I < NT; I += RPW * BIG_NW) {
+    for (int I = kend + wave; I < NT && !(MHE_BIG_KO & 16); I += RPW * BIG_NW) {
       const bool two = RPW == 2 && I + BIG_NW < NT;
       const int I2 = two ? I + BIG_NW : I;
       for (int kk = 0; kk < kb; ++kk) {
@@ -1126,7 +1194,7 @@ __global__ __launch_bounds__(BIG_NTHREADS, BIG_JB == 8 ? 2 : 4) void k_big_chol(
     return;
   }
   // backward: delta_k = L_kk^-T (y_k - sum_{I>k} L_Ik^T delta_I), delta in place in YV
-  for (int k = NT - 1; k >= 0; --k) {
+  for (int k = NT - 1; k >= 0 && !(MHE_BIG_KO & 32); --k) {
     double pv = 0.0;
     for (int I = k + 1 + wave; I < NT; I += BIG_NW) {
       const double* L = H + (size_t)big_tile_index(I, k, NT) * 256;
@@ -1364,7 +1432,7 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_border(BigArgs a) {
 template <int n>
 __global__ __launch_bounds__(256) void k_big_update(BigArgs a) {
   const int b = blockIdx.x;
-  if (a.state[b] != BIG_RUNNING) return;
+  if (a.state[b] != BIG_RUNNING || MHE_BIG_KO) return;  // (timing probes: X frozen)
   const BigWs WL = big_ws_layout(a.P, a.M, n, a.NT, a.nz, a.nc);
   const double* YV = a.ws + (size_t)b * a.ws_stride + WL.YV;
   double* X = a.X + (size_t)b * a.P * n;

@@ -2113,9 +2113,16 @@ int launch_big(const mhe_dims* dm, BigArgs& A, int batch, int max_iter, hipStrea
     const size_t nx = (size_t)batch * A.P * A.n;
     hipLaunchKernelGGL(k_big_project<DYN::n>, dim3((unsigned)((nx + 255) / 256)), dim3(256), 0, st, A, batch);
   }
+  // k_big_assemble: per tile position ceil(nchl / WPB) workgroups of WPB live pair chunks
+  // (the epoch GEMM's operands staged through LDS, big_asm_lds), then the other chunks
+  // WPB (position, chunk) items per workgroup
+  const int asm_wpb = A.nchl > 0 ? (A.nchl < 4 ? A.nchl : 4) : (A.nch < 4 ? A.nch : 4);
+  const int asm_blocks = npos * ((A.nchl + asm_wpb - 1) / asm_wpb) + (npos * (A.nch - A.nchl) + asm_wpb - 1) / asm_wpb;
+  const int asm_lds = big_asm_lds(asm_wpb) * (int)sizeof(double);
   for (int it = 0; it < max_iter; ++it) {
     hipLaunchKernelGGL((k_big_resid<DYN, MEAS>), dim3(batch), dim3(BIG_NTHREADS), 0, st, A, 0);
-    hipLaunchKernelGGL((k_big_assemble<DYN, MEAS>), dim3((npos * A.nch + 3) / 4, batch), dim3(256), 0, st, A);
+    hipLaunchKernelGGL((k_big_assemble<DYN, MEAS>), dim3(asm_blocks, batch), dim3(64 * asm_wpb), asm_lds, st,
+                       A);
     hipLaunchKernelGGL(chol, dim3(batch), dim3(BIG_NTHREADS), smem, st, A);
     if (K > 0) hipLaunchKernelGGL((k_big_border<DYN::n, MEAS::p>), dim3(batch), dim3(BIG_NTHREADS), smem_b, st, A);
     if (bounded)

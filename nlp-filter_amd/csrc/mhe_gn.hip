@@ -85,9 +85,11 @@ __global__ void k_big_consts(int P, int M, int n, int p, const double* D, const 
     const int k = e / P, j = e % P;
     oD[e] = D[e];
     oDt[j * P + k] = D[e];
-    // (D^T C D)[k][j] with C = diag(cw): element (row k, col j)
+    // (D^T C D)[k][j] with C = diag(cw): element (row k, col j), formed in the same order
+    // for (k, j) and (j, k) -- exactly symmetric, so k_big_assemble may read either
+    const int lo = k < j ? k : j, hi = k < j ? j : k;
     double s = 0.0;
-    for (int t = 0; t < P; ++t) s += D[t * P + k] * cw[t] * D[t * P + j];
+    for (int t = 0; t < P; ++t) s += D[t * P + lo] * cw[t] * D[t * P + hi];
     oDCD[e] = s;
   }
   for (int e = gid; e < P; e += stride) ((double*)(cbuf + CL.cw))[e] = cw[e];

@@ -1,9 +1,7 @@
 #!/bin/bash
-# Knock-out builds of the large-system Cholesky (timing probes only; results wrong by design):
+# Knock-out builds of the large-system Cholesky (timing probes only; results wrong by design,
+# X frozen so every iteration solves the same system):
 #   tools/ko_big.sh <mask> -> tools/libmhe_kob<mask>.so   (MHE_LIB=... python tools/bench_big.py)
+# mask bits: mhe_big.h MHE_BIG_KO; 64 = nothing knocked out (the baseline with X frozen)
 set -e
-M=$1
-C=/root/repo/nlp-filter_amd/csrc
-/opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -fPIC -I/root/repo/include -I$C -DMHE_BIG_KO=$M \
-  -c $C/mhe_gn.hip -o /tmp/kob$M.o
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o /root/repo/tools/libmhe_kob$M.so /tmp/kob$M.o $C/build/mhe_ekf.o $C/build/mhe_ls.o
+bash "$(dirname "$0")/build_variant.sh" kob$1 "-DMHE_BIG_KO=$1"

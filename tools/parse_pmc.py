@@ -65,6 +65,22 @@ summary = {
     "note": "2*FETCH_SIZE + WRITE_SIZE (KB), gfx950 FETCH_SIZE halving corrected; 8-B scattered reads are "
             "uncalibrated (MI355X_MICROARCH.md §HBM); Infinity-Cache hits are counted",
 }
+# the kernel's launch durations from the trace pass, split into the bench's warm-up launches
+# and its timed launches: bench.py's kernel_ms (HIP events around the timed launches) and
+# the rocprof average over those same launches are one basis
+durs = []
+for f in glob.glob(os.path.join(out, f"prof_{tag}_trace", "**", "*kernel_trace.csv"), recursive=True):
+    for r in csv.DictReader(open(f)):
+        if "k_gn<mhe::DynVanDerPol" in r.get("Kernel_Name", "") and "MeasFullState" in r["Kernel_Name"]:
+            durs.append((int(r["Dispatch_Id"]), (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6))
+durs = [d for _, d in sorted(durs)]
+warm = int(os.environ.get("PROF_WARMUP", "2"))
+if durs:
+    summary["trace_launches"] = len(durs)
+    summary["trace_ms_all_launches"] = sum(durs) / len(durs)
+    timed = durs[warm:] if len(durs) > warm else durs
+    summary["trace_ms_timed_launches"] = sum(timed) / len(timed)
+    summary["trace_ms_first_launch"] = durs[0]
 os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
 with open(os.path.join(ROOT, "profiles", "pmc_summary.json"), "w") as f:
     json.dump(summary, f, indent=1)
