@@ -1077,29 +1077,52 @@ __global__ __launch_bounds__(BIG_NTHREADS, BIG_JB == 8 ? 2 : 4) void k_big_chol(
     // +2 %, C5 +0.7 %); the 4-wide one keeps one row per wave (the second row's registers
     // spill there: C3 -0.9 %).  Unused second-row work is dead code at JB = 4.
     constexpr int RPW = BIG_JB == 8 ? 2 : 1;
+    // 8-wide instance: loads one step ahead -- the rows' next A_Ik tiles during tile kk, the
+    // next L_Ik' during in-block step kp (C4 -0.4 %); the 4-wide one loads at the point of
+    // use (the prefetch registers add spills there: C3 +1.6 %, profiles/r04_ab_big_rows_prefetch.txt).
+    constexpr bool RPF = BIG_JB == 8;
     for (int I = kend + wave; I < NT && !(MHE_BIG_KO & 16); I += RPW * BIG_NW) {
       const bool two = RPW == 2 && I + BIG_NW < NT;
       const int I2 = two ? I + BIG_NW : I;
+      d4 an, an2;  // A_Ik^T of the next tile, k-major (= row-major A_Ik read transposed)
+      auto load_a = [&](int kk) {
+        const double* A1 = H + (size_t)big_tile_index(I, k0 + kk, NT) * 256;
+        const double* A2 = H + (size_t)big_tile_index(I2, k0 + kk, NT) * 256;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          an[r] = A1[(lane & 15) * 16 + 4 * r + (lane >> 4)];
+          an2[r] = A2[(lane & 15) * 16 + 4 * r + (lane >> 4)];
+        }
+      };
+      if (RPF) load_a(0);
       for (int kk = 0; kk < kb; ++kk) {
         double* Ak = H + (size_t)big_tile_index(I, k0 + kk, NT) * 256;
         double* Ak2 = H + (size_t)big_tile_index(I2, k0 + kk, NT) * 256;
-        d4 c, c2;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          c[r] = Ak[(lane & 15) * 16 + 4 * r + (lane >> 4)];
-          c2[r] = Ak2[(lane & 15) * 16 + 4 * r + (lane >> 4)];
-        }
-        for (int kp = 0; kp < kk && !(MHE_BIG_KO & 2); ++kp) {
-          const double* Lk = LB + (kk * (kk - 1) / 2 + kp) * 256;
-          const double* LI = H + (size_t)big_tile_index(I, k0 + kp, NT) * 256;
-          const double* LI2 = H + (size_t)big_tile_index(I2, k0 + kp, NT) * 256;
-          double lk[4], li[4], li2[4];
+        if (!RPF) load_a(kk);
+        d4 c = an, c2 = an2;
+        if (RPF && kk + 1 < kb) load_a(kk + 1);
+        double ln[4], ln2[4];  // L_Ik' of the next in-block step
+        auto load_l = [&](int kp) {
+          const double* L1 = H + (size_t)big_tile_index(I, k0 + kp, NT) * 256;
+          const double* L2 = H + (size_t)big_tile_index(I2, k0 + kp, NT) * 256;
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            lk[r] = Lk[64 * r + lane];
-            li[r] = LI[64 * r + lane];
-            li2[r] = LI2[64 * r + lane];
+            ln[r] = L1[64 * r + lane];
+            ln2[r] = L2[64 * r + lane];
           }
+        };
+        if (RPF && kk > 0) load_l(0);
+        for (int kp = 0; kp < kk && !(MHE_BIG_KO & 2); ++kp) {
+          const double* Lk = LB + (kk * (kk - 1) / 2 + kp) * 256;
+          double lk[4], li[4], li2[4];
+          if (!RPF) load_l(kp);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            li[r] = ln[r];
+            li2[r] = ln2[r];
+            lk[r] = Lk[64 * r + lane];
+          }
+          if (RPF && kp + 1 < kk) load_l(kp + 1);
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             c = __builtin_amdgcn_mfma_f64_16x16x4f64(lk[r], li[r], c, 0, 0, MFMA_NEG_A);
@@ -1193,16 +1216,51 @@ __global__ __launch_bounds__(BIG_NTHREADS, BIG_JB == 8 ? 2 : 4) void k_big_chol(
     if (threadIdx.x == 0) a.state[b] = MHE_STATUS_NOT_SPD;
     return;
   }
-  // backward: delta_k = L_kk^-T (y_k - sum_{I>k} L_Ik^T delta_I), delta in place in YV
+  // backward: delta_k = L_kk^-T (y_k - sum_{I>k} L_Ik^T delta_I), delta in place in YV.
+  // A chain of NT steps with two barriers each, so nothing on it waits for HBM: every
+  // wave loads its first BWD_PF tiles of column k - 1 (and wave 0 its four L_kk^-T
+  // entries per lane) during step k; y / delta live in LDS (the slab region, free now)
+  // when they fit, the global YV copy is written alongside for k_big_update.
+  constexpr int BWD_PF = BIG_JB == 8 ? 4 : 2;
+  const bool yl = NT * 16 <= big_slab_doubles(BIG_JB);
+  double* yb = yl ? LJ : YV;
+  if (yl) {
+    for (int e = threadIdx.x; e < NT * 16; e += BIG_NTHREADS) LJ[e] = YV[e];
+    __syncthreads();
+  }
+  const int bc = lane & 15, bg = lane >> 4;
+  double cur[BWD_PF][4], nxt[BWD_PF][4], lt[4], ltn[4];
+  auto load_col = [&](int k, double (&dst)[BWD_PF][4], double (&l4)[4]) {
+#pragma unroll
+    for (int m = 0; m < BWD_PF; ++m) {
+      const int I = k + 1 + wave + BIG_NW * m;
+      if (I < NT) {
+        const double* L = H + (size_t)big_tile_index(I, k, NT) * 256;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dst[m][r] = L[bc * 16 + bg + 4 * r];  // L_Ik[tr][bc], k-major tile
+      }
+    }
+    if (wave == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) l4[i] = LTg[(size_t)k * DTS + bc * LIS + 4 * bg + i];
+    }
+  };
+  if (!(MHE_BIG_KO & 32)) load_col(NT - 1, cur, lt);
   for (int k = NT - 1; k >= 0 && !(MHE_BIG_KO & 32); --k) {
+    if (k > 0) load_col(k - 1, nxt, ltn);  // in flight during this step
     double pv = 0.0;
-    for (int I = k + 1 + wave; I < NT; I += BIG_NW) {
+#pragma unroll
+    for (int m = 0; m < BWD_PF; ++m) {
+      const int I = k + 1 + wave + BIG_NW * m;
+      if (I < NT) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pv += cur[m][r] * yb[16 * I + bg + 4 * r];
+      }
+    }
+    for (int I = k + 1 + wave + BIG_NW * BWD_PF; I < NT; I += BIG_NW) {  // past the prefetched tiles (C4, C5)
       const double* L = H + (size_t)big_tile_index(I, k, NT) * 256;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int tr = (lane >> 4) + 4 * r;
-        pv += L[(lane & 15) * 16 + tr] * YV[16 * I + tr];  // L_Ik[tr][lane & 15], k-major tile
-      }
+      for (int r = 0; r < 4; ++r) pv += L[bc * 16 + bg + 4 * r] * yb[16 * I + bg + 4 * r];
     }
     pv += __shfl_xor(pv, 16);
     pv += __shfl_xor(pv, 32);
@@ -1210,17 +1268,28 @@ __global__ __launch_bounds__(BIG_NTHREADS, BIG_JB == 8 ? 2 : 4) void k_big_chol(
     __syncthreads();
     if (wave == 0) {
       if (lane < 16) {
-        double rhs = YV[16 * k + lane];
+        double rhs = yb[16 * k + lane];
         for (int w = 0; w < BIG_NW; ++w) rhs -= PART[w * 16 + lane];
         YL[lane] = rhs;
       }
-      for (int e = lane; e < DTS; e += 64) DT[e] = LTg[(size_t)k * DTS + e];
       wave_lds_sync();
-      block_back(DT, YL, lane);
-      wave_lds_sync();
-      if (lane < 16) YV[16 * k + lane] = YL[lane];
+      // delta_k = L_kk^-T rhs: lane (c, g) the four terms 4g .. 4g + 3 of row c
+      double sd = 0.0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sd = fma(lt[i], YL[4 * bg + i], sd);
+      const double dv = rows4_sum(sd);
+      if (lane < 16) {
+        yb[16 * k + lane] = dv;
+        if (yl) YV[16 * k + lane] = dv;
+      }
     }
     __syncthreads();
+#pragma unroll
+    for (int m = 0; m < BWD_PF; ++m)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) cur[m][r] = nxt[m][r];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) lt[i] = ltn[i];
   }
 }
 
