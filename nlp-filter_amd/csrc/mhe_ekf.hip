@@ -119,6 +119,7 @@ struct EkfDiscreteVehicle {
 template <bool with_bias>
 struct EkfMultiPseudorange {
   static constexpr int q = 3;
+  static constexpr int lane_minw = with_bias ? 2 : 4;  // k_ekf_lane waves per SIMD (no spills)
   template <int n>
   __device__ static void row(const double* x, const double* par, int i, int nz, double& h, double* H) {
     if (with_bias && i == nz - 1) {
@@ -143,6 +144,7 @@ struct EkfMultiPseudorange {
 // 5-column Jacobian scattered back to the 9-state (columns 0, 1, 8, 6, 7).
 struct EkfVehicleSensors {
   static constexpr int q = 3;
+  static constexpr int lane_minw = 2;
   template <int n>
   __device__ static void row(const double* x, const double* par, int /*i*/, int /*nz*/, double& h, double* H) {
     const double l0 = par[0] - x[0], l1 = par[1] - x[1], l2 = par[2] - x[8];
@@ -360,7 +362,7 @@ __global__ __launch_bounds__(NWF * 64) void k_ekf(EkfArgs a) {
 // The symmetric form reads S[r][c] = S[c][r] = stored (min, max) entry.
 template <int n>
 struct LaneS {
-  static constexpr bool sym = n > 6;
+  static constexpr bool sym = true;
   static constexpr int size = sym ? n * (n + 1) / 2 : n * n;
   static constexpr int at(int r, int c) {
     return sym ? (r <= c ? r * n - r * (r - 1) / 2 + (c - r) : c * n - c * (c - 1) / 2 + (r - c)) : r * n + c;
@@ -368,7 +370,7 @@ struct LaneS {
 };
 
 template <class DYN, class MEAS>
-__global__ __launch_bounds__(256) void k_ekf_lane(EkfArgs a) {
+__global__ __launch_bounds__(256, MEAS::lane_minw) void k_ekf_lane(EkfArgs a) {
   constexpr int n = DYN::n, m = DYN::m, q = MEAS::q;
   using LS = LaneS<n>;
   const int b = blockIdx.x * blockDim.x + threadIdx.x;

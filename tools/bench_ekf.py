@@ -96,7 +96,7 @@ from oracle import ekf as oekf  # noqa: E402
 if LAYOUT == "batch_inner":
     U, Z, nz = (np.moveaxis(x, -1, 0) for x in (U, Z, nz))
 nb, t0 = 0, time.perf_counter()
-while time.perf_counter() - t0 < 5.0:
+while time.perf_counter() - t0 < (0.0 if os.environ.get("NO_CPU") else 5.0):
     b = nb % B
     f = oekf.EKF(oekf.gnss_pos_and_bias, oekf.multi_pseudorange, mu0[b], S0[b])
     for k in range(T):

@@ -75,7 +75,7 @@ rate = B * T / (ms * 1e-3)
 # CPU baseline: the oracle EKF, one core, bounded sample
 from oracle import ekf as oe  # noqa: E402
 nb, t0 = 0, time.perf_counter()
-while time.perf_counter() - t0 < 10.0 and nb < 64:
+while time.perf_counter() - t0 < (0.0 if os.environ.get("NO_CPU") else 10.0) and nb < 64:
     f = oe.EKF(oe.discrete_vehicle_dynamics, oe.vehicle_sensors_model, mu0[nb], S0[nb])
     for k in range(T):
         ns = int(fx["nz"][k])
