@@ -249,6 +249,10 @@ def main():
                     # average over the profiled bench's timed launches (its warm-up excluded)
                     rec["roofline"]["kernel_ms_rocprof_timed"] = ps["trace_ms_timed_launches"]
                     rec["roofline"]["kernel_ms_rocprof_all"] = ps["trace_ms_all_launches"]
+                    # frac on the rocprof basis (the tracer's own timing of those launches,
+                    # profiles/<tag>_kernel_stats.csv), next to frac on the HIP-event basis
+                    rec["roofline"]["frac_rocprof_timed"] = (fl / (ps["trace_ms_timed_launches"] * 1e-3) / 1e12
+                                                             / FP64_PEAK_TFLOPS)
             elif same:
                 rec["roofline"]["traffic_note"] = (f"profiles/pmc_summary.json measured build {ps.get('lib_sha')}, "
                                                    f"not this libmhe.so ({lib_digest()}): traffic omitted")

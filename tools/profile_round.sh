@@ -10,3 +10,6 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/p
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_${TAG}_write -o run -- $B > gpurun_out/prof_${TAG}_write.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVE_CYCLES --output-format csv -d gpurun_out/prof_${TAG}_sq -o run -- $B > gpurun_out/prof_${TAG}_sq.log 2>&1
 python tools/parse_pmc.py "$TAG"
+# profiles/ on the box is not copied back: hand the summary and stats over through gpurun_out/
+cp profiles/pmc_summary.json "gpurun_out/pmc_summary_${TAG}.json"
+cp "profiles/${TAG}_kernel_stats.csv" "gpurun_out/${TAG}_kernel_stats.csv"
