@@ -1491,8 +1491,11 @@ __device__ __forceinline__ int opaque_s(int x) {
 #define FCL const_layout(opaque_s(a.P), opaque_s(a.M), n, MEAS::p, opaque_s(a.NT))
 #define FSL smem_layout(opaque_s(a.P), opaque_s(a.M), n, opaque_s(a.NT), !MEAS::LINEAR)
 
-template <class DYN, class MEAS, int SLOTS, int mode, bool HUBER = false>
-__global__ __launch_bounds__(NTHREADS, MHE_GN_MINW) void k_gn(GnArgs a) {  // 2nd arg: min waves per SIMD (8 waves: 2 WGs per CU)
+// MINW (launch bounds' 2nd argument): min waves per SIMD -- 4 = two workgroups (trajectories)
+// per CU, 128 VGPRs; 2 = the small-batch instance (batch <= CUs: one workgroup per CU
+// anyway), which may use 256 VGPRs
+template <class DYN, class MEAS, int SLOTS, int mode, bool HUBER = false, int MINW = MHE_GN_MINW>
+__global__ __launch_bounds__(NTHREADS, MINW) void k_gn(GnArgs a) {
   constexpr int n = DYN::n;
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const ConstLayout CL = const_layout(a.P, a.M, n, MEAS::p, a.NT);
@@ -2048,6 +2051,18 @@ struct PairOps {
   int (*resjac)(ResjacArgs& a, int batch, hipStream_t st);
 };
 
+// compute units of the current device (cached per device)
+inline int device_cus() {
+  static int cus[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cus[dev] == 0) {
+    int v = 0;
+    cus[dev] = hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0 ? v : 256;
+  }
+  return cus[dev];
+}
+
 template <class DYN, class MEAS>
 int launch_gn(const mhe_dims* dm, GnArgs& a, int batch, int mode, hipStream_t st) {
   if constexpr (MEAS::MIXED) {
@@ -2059,7 +2074,12 @@ int launch_gn(const mhe_dims* dm, GnArgs& a, int batch, int mode, hipStream_t st
     void (*kern)(GnArgs) = nullptr;
     const bool huber = dm->dyn_cost == MHE_COST_HUBER;
     if (bounded) kern = huber ? k_gn_bounded<DYN, MEAS, MAX_SLOTS, true> : k_gn_bounded<DYN, MEAS, MAX_SLOTS>;
-    else if (mode == MODE_SOLVE) kern = huber ? k_gn<DYN, MEAS, MAX_SLOTS, MODE_SOLVE, true> : k_gn<DYN, MEAS, MAX_SLOTS, MODE_SOLVE>;
+    else if (mode == MODE_SOLVE)
+      // a batch that gives each CU at most one trajectory runs the instance without the
+      // two-workgroups-per-CU register cap (C2 strong scaling at 4-8 GPUs: 256 / 128 per GPU)
+      kern = huber ? k_gn<DYN, MEAS, MAX_SLOTS, MODE_SOLVE, true>
+             : batch <= device_cus() ? k_gn<DYN, MEAS, MAX_SLOTS, MODE_SOLVE, false, 2>
+                                     : k_gn<DYN, MEAS, MAX_SLOTS, MODE_SOLVE>;
     else if (mode == MODE_ASSEMBLE)
       kern = huber ? k_gn<DYN, MEAS, MAX_SLOTS, MODE_ASSEMBLE, true> : k_gn<DYN, MEAS, MAX_SLOTS, MODE_ASSEMBLE>;
     else kern = k_gn<DYN, MEAS, MAX_SLOTS, MODE_LINSOLVE>;
