@@ -174,3 +174,18 @@ def test_bitwise_deterministic_full_occupancy():
     d1, s1 = s.chol_solve(H, g)
     d2, s2 = s.chol_solve(H, g)
     assert torch.equal(d1, d2) and (s1.cpu().numpy() == 0).all()
+
+
+def test_small_batch_instance_matches_full_occupancy_instance():
+    """launch_gn runs the small-batch instance of k_gn (launch bounds of 2 waves per SIMD)
+    when the batch gives each CU at most one trajectory, and the two-workgroups-per-CU
+    instance otherwise.  They differ only in register allocation, so the same trajectories
+    solved in a small batch and inside a large one agree bit for bit."""
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    w = configs.make_c2(B=2 * cus + 8)
+    s = solver.from_workload(w)
+    big = [t.cpu().numpy() for t in s.solve(w.X_init, w.U, w.Y, max_iter=4, tol=0.0)]
+    sub = slice(0, 96)
+    small = [t.cpu().numpy() for t in s.solve(w.X_init[sub], w.U, w.Y[sub], max_iter=4, tol=0.0)]
+    for a, b in zip(small, big):
+        assert np.array_equal(a, b[sub])
