@@ -17,7 +17,9 @@ J^T W J / J^T W r assembly, register-tiled Cholesky, two triangular solves,
 update.  value = (all ranks) sum of B_r * P * GN_ITERS * K / max-rank wall.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu] [--global-batch G] [--weak [--batch B]]
-N > 1 is launched by torch.distributed.run (RANK/LOCAL_RANK/WORLD_SIZE env).
+N > 1: under torch.distributed.run (RANK/LOCAL_RANK/WORLD_SIZE set) each process is one
+rank; run plainly, bench.py starts the N ranks itself (mhe.launch, before any GPU call)
+and exits with their code.
 """
 import argparse
 import json
@@ -148,6 +150,12 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=1024)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     args = ap.parse_args()
+
+    # `python bench.py --gpus N` on its own: start the N ranks here, before anything
+    # touches the GPU (mhe.launch imports no torch), and exit with their code.  Under
+    # torch.distributed.run (WORLD_SIZE set) this returns at once.
+    from mhe import launch
+    launch.relaunch_if_needed(args.gpus)
 
     import torch
 

@@ -111,7 +111,7 @@ extern "C" {
  * the size queries) unless it equals this build's sizeof -- a binding that
  * declares an older or truncated struct is refused before any later field is
  * read.  (mhe/_lib.py sets it in the ctypes constructors.) */
-#define MHE_ABI_VERSION 4
+#define MHE_ABI_VERSION 5
 
 typedef struct mhe_dims {
   int32_t struct_size;  /* = sizeof(mhe_dims)                                */
@@ -336,6 +336,8 @@ int mhe_resjac(const mhe_dims* dims, const void* const_buf, int32_t batch, const
  * Kernel-level parity: assemble the GN normal equations at X.
  *   H (B,dp,dp) full symmetric (dp = mhe_padded_dim; padding rows = identity),
  *   g (B,dp) gradient J^T W r (padding 0), cost (B).
+ * Register-resident path only (MHE_ERR_UNSUPPORTED on the large-system path, which
+ * needs a workspace: mhe_assemble_ws / mhe_chol_solve_ws below).
  */
 int mhe_assemble(const mhe_dims* dims, const void* const_buf, int32_t batch,
                  const double* X, const double* U, int64_t u_bstride,
@@ -351,6 +353,35 @@ int mhe_assemble(const mhe_dims* dims, const void* const_buf, int32_t batch,
 int mhe_chol_solve(const mhe_dims* dims, const void* const_buf, int32_t batch,
                    const double* H, const double* g, double* delta, int32_t* status,
                    void* stream);
+
+/*
+ * Both kernel-level parity entry points for EVERY path (ABI v5): on the register-
+ * resident path they are mhe_assemble / mhe_chol_solve (workspace ignored, status
+ * set to 0 by the assembly); on the large-system path (C3-C5, mhe_workspace_bytes > 0)
+ * they run the solve's own kernels over a caller-owned workspace of
+ * >= mhe_workspace_bytes(dims, batch) bytes:
+ *   mhe_assemble_ws    k_big_resid + k_big_assemble at X, then H and g copied out of
+ *                      the kernels' component-major tiles into the SAME dense node-major
+ *                      layout as mhe_assemble: H (B,dp,dp), g (B,dp), dp = mhe_padded_dim
+ *                      = n * Pp, row j*n + c for node j < Pp (the first P*n rows are the
+ *                      oracle's order; padding nodes last: identity block, zero coupling,
+ *                      zero gradient), cost (B), status (B): 0, or
+ *                      MHE_STATUS_BAD_CONSTANTS (outputs NaN).  The plain GN system
+ *                      (bounds are a solve-time reduction); n_extra / n_eq > 0:
+ *                      MHE_ERR_UNSUPPORTED (the bordered system is not exported).
+ *   mhe_chol_solve_ws  H (lower triangle read, node-major as above) and g into the
+ *                      tiles, k_big_chol (blocked Cholesky + both triangular solves),
+ *                      delta = -H^-1 g (B,dp) node-major; status 0, MHE_STATUS_NOT_SPD
+ *                      (non-positive or non-finite pivot; delta NaN) or BAD_CONSTANTS.
+ */
+int mhe_assemble_ws(const mhe_dims* dims, const void* const_buf, int32_t batch,
+                    const double* X, const double* U, int64_t u_bstride,
+                    const double* Y, const double* PAR, int64_t par_bstride,
+                    const double* x0, double* H, double* g, double* cost, int32_t* status,
+                    void* workspace, size_t workspace_bytes, void* stream);
+int mhe_chol_solve_ws(const mhe_dims* dims, const void* const_buf, int32_t batch,
+                      const double* H, const double* g, double* delta, int32_t* status,
+                      void* workspace, size_t workspace_bytes, void* stream);
 
 /* ------------------------------------------------------------------------
  * Batched extended Kalman filter.

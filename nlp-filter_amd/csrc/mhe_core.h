@@ -2049,6 +2049,8 @@ struct PairOps {
   int (*big)(const mhe_dims* dm, BigArgs& A, int batch, int max_iter, hipStream_t st);
   // kernel-level parity: residuals and Jacobians per node / row (mhe_resjac)
   int (*resjac)(ResjacArgs& a, int batch, hipStream_t st);
+  // kernel-level parity of the large-system path: one stage (BIG_STAGE_*) on the workspace
+  int (*big_stage)(const mhe_dims* dm, BigArgs& A, int batch, int stage, hipStream_t st);
 };
 
 // compute units of the current device (cached per device)
@@ -2104,20 +2106,64 @@ int launch_build_cc(const mhe_dims* dm, int NT, const double* D, const double* c
   }
 }
 
-template <class DYN, class MEAS>
-int launch_big(const mhe_dims* dm, BigArgs& A, int batch, int max_iter, hipStream_t st) {
-  const int npos = A.NTc * (A.NTc + 1) / 2;
-  big_pair_plan(A, BigGSupport<MEAS>::get(A.idx, A.n));
+// The factorization instance of the large-system path and its LDS bytes: left-looking
+// block-column updates (default; 38 % less HBM traffic than the right-looking trailing
+// update, C3 +5 %, C4 +7.5 %, C5 +8 %); the right-looking form (bitwise-identical
+// iterates, tests/test_gpu_big.py) only when a caller selected it explicitly with
+// mhe_set_option(MHE_OPT_BIG_RIGHT_LOOKING, 1)
+inline int big_chol_kernel(const BigArgs& A, void (**chol)(BigArgs)) {
   const bool wide = A.NT >= BIG_WIDE_NT;
   const int smem = big_chol_lds(wide ? 8 : 4) * (int)sizeof(double);
-  // left-looking block-column updates (default; 38 % less HBM traffic than the
-  // right-looking trailing update, C3 +5 %, C4 +7.5 %, C5 +8 %); the right-looking form
-  // (bitwise-identical iterates, tests/test_gpu_big.py) only when a caller selected it
-  // explicitly with mhe_set_option(MHE_OPT_BIG_RIGHT_LOOKING, 1)
   const bool ll = g_opt_big_right_looking == 0;
-  void (*chol)(BigArgs) = wide ? (ll ? k_big_chol<8, true> : k_big_chol<8>) : (ll ? k_big_chol<4, true> : k_big_chol<4>);
-  if (hipFuncSetAttribute((const void*)chol, hipFuncAttributeMaxDynamicSharedMemorySize, smem) != hipSuccess)
-    return MHE_ERR_HIP;
+  *chol = wide ? (ll ? k_big_chol<8, true> : k_big_chol<8>) : (ll ? k_big_chol<4, true> : k_big_chol<4>);
+  if (hipFuncSetAttribute((const void*)*chol, hipFuncAttributeMaxDynamicSharedMemorySize, smem) != hipSuccess)
+    return -1;
+  return smem;
+}
+
+// k_big_assemble's launch shape: per tile position ceil(nchl / WPB) workgroups of WPB
+// live pair chunks (the epoch GEMM's operands staged through LDS, big_asm_lds), then the
+// other chunks WPB (position, chunk) items per workgroup
+struct BigAsmShape {
+  int wpb, blocks, lds;
+};
+inline BigAsmShape big_asm_shape(const BigArgs& A) {
+  const int npos = A.NTc * (A.NTc + 1) / 2;
+  BigAsmShape s;
+  s.wpb = A.nchl > 0 ? (A.nchl < 4 ? A.nchl : 4) : (A.nch < 4 ? A.nch : 4);
+  s.blocks = npos * ((A.nchl + s.wpb - 1) / s.wpb) + (npos * (A.nch - A.nchl) + s.wpb - 1) / s.wpb;
+  s.lds = big_asm_lds(s.wpb) * (int)sizeof(double);
+  return s;
+}
+
+// Kernel-level parity stages of the large-system path (mhe_assemble_ws /
+// mhe_chol_solve_ws): BIG_STAGE_ASSEMBLE runs k_big_resid + k_big_assemble at A.X (H
+// tiles and BV = -g in the workspace, cost), BIG_STAGE_FACTOR runs k_big_chol on the
+// workspace's tiles and BV (delta in YV).  The state words are set by the caller.
+constexpr int BIG_STAGE_ASSEMBLE = 0, BIG_STAGE_FACTOR = 1;
+template <class DYN, class MEAS>
+int launch_big_stage(const mhe_dims* dm, BigArgs& A, int batch, int stage, hipStream_t st) {
+  (void)dm;
+  if (stage == BIG_STAGE_ASSEMBLE) {
+    big_pair_plan(A, BigGSupport<MEAS>::get(A.idx, A.n));
+    const BigAsmShape sh = big_asm_shape(A);
+    hipLaunchKernelGGL((k_big_resid<DYN, MEAS>), dim3(batch), dim3(BIG_NTHREADS), 0, st, A, 0);
+    hipLaunchKernelGGL((k_big_assemble<DYN, MEAS>), dim3(sh.blocks, batch), dim3(64 * sh.wpb), sh.lds, st, A);
+  } else {
+    void (*chol)(BigArgs) = nullptr;
+    const int smem = big_chol_kernel(A, &chol);
+    if (smem < 0) return MHE_ERR_HIP;
+    hipLaunchKernelGGL(chol, dim3(batch), dim3(BIG_NTHREADS), smem, st, A);
+  }
+  return hipGetLastError() == hipSuccess ? MHE_OK : MHE_ERR_HIP;
+}
+
+template <class DYN, class MEAS>
+int launch_big(const mhe_dims* dm, BigArgs& A, int batch, int max_iter, hipStream_t st) {
+  big_pair_plan(A, BigGSupport<MEAS>::get(A.idx, A.n));
+  void (*chol)(BigArgs) = nullptr;
+  const int smem = big_chol_kernel(A, &chol);
+  if (smem < 0) return MHE_ERR_HIP;
   const int K = A.nz + A.nc;
   const int smem_b = (K * K + 2 * K) * (int)sizeof(double);
   if (K > 0 && hipFuncSetAttribute((const void*)k_big_border<DYN::n, MEAS::p>,
@@ -2133,16 +2179,10 @@ int launch_big(const mhe_dims* dm, BigArgs& A, int batch, int max_iter, hipStrea
     const size_t nx = (size_t)batch * A.P * A.n;
     hipLaunchKernelGGL(k_big_project<DYN::n>, dim3((unsigned)((nx + 255) / 256)), dim3(256), 0, st, A, batch);
   }
-  // k_big_assemble: per tile position ceil(nchl / WPB) workgroups of WPB live pair chunks
-  // (the epoch GEMM's operands staged through LDS, big_asm_lds), then the other chunks
-  // WPB (position, chunk) items per workgroup
-  const int asm_wpb = A.nchl > 0 ? (A.nchl < 4 ? A.nchl : 4) : (A.nch < 4 ? A.nch : 4);
-  const int asm_blocks = npos * ((A.nchl + asm_wpb - 1) / asm_wpb) + (npos * (A.nch - A.nchl) + asm_wpb - 1) / asm_wpb;
-  const int asm_lds = big_asm_lds(asm_wpb) * (int)sizeof(double);
+  const BigAsmShape sh = big_asm_shape(A);
   for (int it = 0; it < max_iter; ++it) {
     hipLaunchKernelGGL((k_big_resid<DYN, MEAS>), dim3(batch), dim3(BIG_NTHREADS), 0, st, A, 0);
-    hipLaunchKernelGGL((k_big_assemble<DYN, MEAS>), dim3(asm_blocks, batch), dim3(64 * asm_wpb), asm_lds, st,
-                       A);
+    hipLaunchKernelGGL((k_big_assemble<DYN, MEAS>), dim3(sh.blocks, batch), dim3(64 * sh.wpb), sh.lds, st, A);
     hipLaunchKernelGGL(chol, dim3(batch), dim3(BIG_NTHREADS), smem, st, A);
     if (K > 0) hipLaunchKernelGGL((k_big_border<DYN::n, MEAS::p>), dim3(batch), dim3(BIG_NTHREADS), smem_b, st, A);
     if (bounded)
@@ -2157,7 +2197,7 @@ int launch_big(const mhe_dims* dm, BigArgs& A, int batch, int max_iter, hipStrea
 template <class DYN, class MEAS>
 const PairOps* pair_ops() {
   static const PairOps ops = {&launch_build_cc<DYN, MEAS>, &launch_gn<DYN, MEAS>, &launch_big<DYN, MEAS>,
-                              &launch_resjac<DYN, MEAS>};
+                              &launch_resjac<DYN, MEAS>, &launch_big_stage<DYN, MEAS>};
   return &ops;
 }
 

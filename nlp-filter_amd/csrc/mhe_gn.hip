@@ -304,7 +304,110 @@ GnArgs make_args(const mhe_dims* dm, const void* cbuf, int NT) {
   return a;
 }
 
+// The large-system path's launch arguments that follow from the dims and the
+// constants / workspace alone (the per-solve pointers are set by the caller).
+BigArgs make_big_args(const mhe_dims* dims, const void* cbuf, int NT, void* workspace) {
+  BigArgs A = {};
+  A.cbuf = (const char*)cbuf;
+  A.P = dims->N + 1; A.M = dims->M; A.n = dims->n; A.Pp = big_pp(A.P); A.NTc = A.Pp / 16; A.NT = NT;
+  A.q = dims->q; A.has_prior = dims->has_prior;
+  for (int i = 0; i < 8; ++i) A.idx[i] = dims->meas_idx[i];
+  A.alpha = 2.0 / dims->T;
+  A.ws = (double*)workspace; A.ws_stride = big_ws_doubles(dims, NT);
+  A.n_bounds = dims->n_bounds;
+  for (int i = 0; i < 8; ++i) {
+    A.bidx[i] = dims->bound_idx[i];
+    A.blb[i] = dims->bound_lb[i];
+    A.bub[i] = dims->bound_ub[i];
+    A.dpar[i] = dims->dyn_par[i];
+  }
+  A.nz = dims->n_extra;
+  A.nc = dims->n_eq;
+  A.huber = dims->dyn_cost == MHE_COST_HUBER;
+  A.huber_delta = dims->huber_delta;
+  A.tag = const_tag(dims, NT);
+  return A;
+}
+
 }  // namespace
+
+// ------------------------------------------------------------ large-system parity I/O
+// mhe_assemble_ws / mhe_chol_solve_ws on the large-system path: the kernels keep H as
+// the lower 16x16 tiles (row-major inside a tile) of the COMPONENT-MAJOR system
+// (unknown (node j, component c) at row c*Pp + j); the caller sees the dense NODE-MAJOR
+// system of mhe_assemble (row j*n + c, j < Pp: the first P*n rows are the oracle's
+// order, padding nodes last).  cm(r) maps a node-major row to its component-major one.
+namespace mhe {
+
+__device__ __forceinline__ int big_cm(int r, int n, int Pp) { return (r % n) * Pp + r / n; }
+
+// state word per trajectory: running, or BAD_CONSTANTS when the buffer's stamp does
+// not match these dims (then nothing of the stage runs and the outputs are NaN)
+__global__ void k_big_parity_init(BigArgs a, int batch) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < batch) {
+    const bool ok = *(const unsigned long long*)a.cbuf == a.tag;
+    a.state[b] = ok ? BIG_RUNNING : MHE_STATUS_BAD_CONSTANTS;
+    if (!ok && a.cost) a.cost[b] = NAN;
+  }
+}
+
+__global__ void k_big_parity_finish(int batch, int* state) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < batch && state[b] == BIG_RUNNING) state[b] = MHE_STATUS_CONVERGED;
+}
+
+// dense node-major H (full, both triangles) and g = -BV from the tiles; grid (x, batch)
+__global__ void k_big_export_hg(BigArgs a, int batch, double* Hout, double* gout) {
+  const int b = blockIdx.y;
+  const int dp = a.n * a.Pp;
+  const BigWs WL = big_ws_layout(a.P, a.M, a.n, a.NT, a.nz, a.nc);
+  const double* ws = a.ws + (size_t)b * a.ws_stride;
+  const bool ok = a.state[b] == BIG_RUNNING;
+  const size_t nel = (size_t)dp * dp;
+  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < nel; e += (size_t)gridDim.x * blockDim.x) {
+    const int r = (int)(e / dp), c = (int)(e % dp);
+    const int R = big_cm(r, a.n, a.Pp), C = big_cm(c, a.n, a.Pp);
+    const int hi = R >= C ? R : C, lo = R >= C ? C : R;
+    const double v = ws[WL.H + (size_t)big_tile_index(hi >> 4, lo >> 4, a.NT) * 256 + (hi & 15) * 16 + (lo & 15)];
+    Hout[(size_t)b * nel + e] = ok ? v : NAN;
+    if (c == 0) gout[(size_t)b * dp + r] = ok ? -ws[WL.BV + R] : NAN;
+  }
+}
+
+// the caller's dense node-major H (lower triangle read) and g into the tiles and BV = -g;
+// grid (lower tiles, batch), one thread per tile element
+__global__ void k_big_import_hg(BigArgs a, int batch, const double* Hin, const double* gin) {
+  const int b = blockIdx.y;
+  const int dp = a.n * a.Pp;
+  const BigWs WL = big_ws_layout(a.P, a.M, a.n, a.NT, a.nz, a.nc);
+  double* ws = a.ws + (size_t)b * a.ws_stride;
+  int t = blockIdx.x, J = 0;  // tile t -> (I, J), I >= J, column-major over the lower triangle
+  while (t >= a.NT - J) {
+    t -= a.NT - J;
+    ++J;
+  }
+  const int I = J + t;
+  const int tr = threadIdx.x >> 4, tc = threadIdx.x & 15;
+  const int R = 16 * I + tr, C = 16 * J + tc;  // component-major
+  const int r = (R % a.Pp) * a.n + R / a.Pp, c = (C % a.Pp) * a.n + C / a.Pp;
+  const int hi = r >= c ? r : c, lo = r >= c ? c : r;  // node-major, lower triangle
+  ws[WL.H + (size_t)blockIdx.x * 256 + threadIdx.x] = Hin[((size_t)b * dp + hi) * dp + lo];
+  if (I == J && tr == 0) ws[WL.BV + 16 * I + tc] = -gin[(size_t)b * dp + (C % a.Pp) * a.n + C / a.Pp];
+}
+
+// delta (node-major) from YV (component-major)
+__global__ void k_big_export_delta(BigArgs a, int batch, double* delta) {
+  const int dp = a.n * a.Pp;
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (long long)batch * dp) return;
+  const int b = (int)(e / dp), r = (int)(e % dp);
+  const BigWs WL = big_ws_layout(a.P, a.M, a.n, a.NT, a.nz, a.nc);
+  const double* ws = a.ws + (size_t)b * a.ws_stride;
+  delta[e] = a.state[b] == BIG_RUNNING ? ws[WL.YV + big_cm(r, a.n, a.Pp)] : NAN;
+}
+
+}  // namespace mhe
 
 #ifdef MHE_DIAG
 extern "C" void mhe_diag_set_buffer(void* p) { g_dbg = (unsigned long long*)p; }
@@ -420,30 +523,12 @@ int mhe_solve(const mhe_dims* dims, const void* const_buf, const mhe_solve_args*
   hipStream_t st = (hipStream_t)stream;
   if (is_big(dims)) {
     if (!g->workspace || g->workspace_bytes < mhe_workspace_bytes(dims, batch)) return MHE_ERR_NULL;
-    BigArgs A = {};
-    A.cbuf = (const char*)const_buf;
-    A.P = dims->N + 1; A.M = dims->M; A.n = dims->n; A.Pp = big_pp(A.P); A.NTc = A.Pp / 16; A.NT = NT;
-    A.q = dims->q; A.has_prior = dims->has_prior;
-    for (int i = 0; i < 8; ++i) A.idx[i] = dims->meas_idx[i];
-    A.alpha = 2.0 / dims->T;
+    BigArgs A = make_big_args(dims, const_buf, NT, g->workspace);
     A.U = g->U; A.ustride = g->u_bstride; A.Y = g->Y; A.PAR = g->PAR; A.pstride = g->par_bstride; A.x0 = g->x0;
     A.Rw = g->Rw; A.rwstride = g->rw_bstride;
     A.X = g->X_out; A.cost = g->cost_out; A.iters = g->iters_out; A.state = g->status_out; A.tol = g->tol;
-    A.ws = (double*)g->workspace; A.ws_stride = big_ws_doubles(dims, NT);
-    A.n_bounds = dims->n_bounds;
-    for (int i = 0; i < 8; ++i) {
-      A.bidx[i] = dims->bound_idx[i];
-      A.blb[i] = dims->bound_lb[i];
-      A.bub[i] = dims->bound_ub[i];
-      A.dpar[i] = dims->dyn_par[i];
-    }
-    A.nz = dims->n_extra;
-    A.nc = dims->n_eq;
     A.Z = g->Z_out;
     A.lam = dims->n_eq > 0 ? g->lambda_out : nullptr;
-    A.huber = dims->dyn_cost == MHE_COST_HUBER;
-    A.huber_delta = dims->huber_delta;
-    A.tag = const_tag(dims, NT);
     if (A.X != g->X0 &&
         hipMemcpyAsync(A.X, g->X0, sizeof(double) * batch * A.P * A.n, hipMemcpyDeviceToDevice, st) != hipSuccess)
       return MHE_ERR_HIP;
@@ -520,6 +605,71 @@ int mhe_chol_solve(const mhe_dims* dims, const void* const_buf, int32_t batch, c
   GnArgs a = make_args(dims, const_buf, NT);
   a.Hin = H; a.gin = g; a.dout = delta; a.status = status;
   return ops->gn(dims, a, batch, MODE_LINSOLVE, (hipStream_t)stream);
+}
+
+int mhe_assemble_ws(const mhe_dims* dims, const void* const_buf, int32_t batch, const double* X, const double* U,
+                    int64_t u_bstride, const double* Y, const double* PAR, int64_t par_bstride, const double* x0,
+                    double* H, double* g, double* cost, int32_t* status, void* workspace, size_t workspace_bytes,
+                    void* stream) {
+  int NT = 0;
+  int rc = check_dims(dims, &NT);
+  if (rc != MHE_OK) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  if (!is_big(dims)) {
+    rc = mhe_assemble(dims, const_buf, batch, X, U, u_bstride, Y, PAR, par_bstride, x0, H, g, cost, stream);
+    if (rc == MHE_OK && status && batch > 0 && hipMemsetAsync(status, 0, sizeof(int32_t) * batch, st) != hipSuccess)
+      return MHE_ERR_HIP;
+    return rc;
+  }
+  if (dims->n_extra > 0 || dims->n_eq > 0) return MHE_ERR_UNSUPPORTED;  // the bordered KKT system is not exported
+  if (batch <= 0) return batch == 0 ? MHE_OK : MHE_ERR_DIMS;
+  if (!const_buf || !X || !H || !g || !cost || !status || (dims->M > 0 && !Y) || (dims->m > 0 && !U) ||
+      (dims->q > 0 && !PAR) || (dims->has_prior && !x0))
+    return MHE_ERR_NULL;
+  if (!workspace || workspace_bytes < mhe_workspace_bytes(dims, batch)) return MHE_ERR_NULL;
+  const PairOps* ops = find_pair(dims);
+  if (!ops) return MHE_ERR_UNSUPPORTED;
+  BigArgs A = make_big_args(dims, const_buf, NT, workspace);
+  A.n_bounds = 0;  // the plain GN system: the projected method's reduction belongs to the solve
+  A.U = U; A.ustride = u_bstride; A.Y = Y; A.PAR = PAR; A.pstride = par_bstride; A.x0 = x0;
+  A.X = const_cast<double*>(X);  // read only by k_big_resid / k_big_assemble
+  A.cost = cost; A.state = status;
+  const int nb = (batch + 255) / 256;
+  hipLaunchKernelGGL(k_big_parity_init, dim3(nb), dim3(256), 0, st, A, batch);
+  rc = ops->big_stage(dims, A, batch, BIG_STAGE_ASSEMBLE, st);
+  if (rc != MHE_OK) return rc;
+  const size_t dp = (size_t)A.n * A.Pp;
+  const size_t gx0 = (dp * dp + 255) / 256;
+  const unsigned gx = (unsigned)(gx0 < 8192 ? gx0 : 8192);
+  hipLaunchKernelGGL(k_big_export_hg, dim3(gx, batch), dim3(256), 0, st, A, batch, H, g);
+  hipLaunchKernelGGL(k_big_parity_finish, dim3(nb), dim3(256), 0, st, batch, status);
+  return hipGetLastError() == hipSuccess ? MHE_OK : MHE_ERR_HIP;
+}
+
+int mhe_chol_solve_ws(const mhe_dims* dims, const void* const_buf, int32_t batch, const double* H, const double* g,
+                      double* delta, int32_t* status, void* workspace, size_t workspace_bytes, void* stream) {
+  int NT = 0;
+  int rc = check_dims(dims, &NT);
+  if (rc != MHE_OK) return rc;
+  if (!is_big(dims)) return mhe_chol_solve(dims, const_buf, batch, H, g, delta, status, stream);
+  if (batch <= 0) return batch == 0 ? MHE_OK : MHE_ERR_DIMS;
+  if (!const_buf || !H || !g || !delta || !status) return MHE_ERR_NULL;
+  if (!workspace || workspace_bytes < mhe_workspace_bytes(dims, batch)) return MHE_ERR_NULL;
+  const PairOps* ops = find_pair(dims);
+  if (!ops) return MHE_ERR_UNSUPPORTED;
+  hipStream_t st = (hipStream_t)stream;
+  BigArgs A = make_big_args(dims, const_buf, NT, workspace);
+  A.n_bounds = 0;
+  A.state = status;
+  const int nb = (batch + 255) / 256;
+  hipLaunchKernelGGL(k_big_parity_init, dim3(nb), dim3(256), 0, st, A, batch);
+  hipLaunchKernelGGL(k_big_import_hg, dim3(NT * (NT + 1) / 2, batch), dim3(256), 0, st, A, batch, H, g);
+  rc = ops->big_stage(dims, A, batch, BIG_STAGE_FACTOR, st);
+  if (rc != MHE_OK) return rc;
+  const long long ne = (long long)batch * A.n * A.Pp;
+  hipLaunchKernelGGL(k_big_export_delta, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, st, A, batch, delta);
+  hipLaunchKernelGGL(k_big_parity_finish, dim3(nb), dim3(256), 0, st, batch, status);
+  return hipGetLastError() == hipSuccess ? MHE_OK : MHE_ERR_HIP;
 }
 
 }  // extern "C"

@@ -81,6 +81,9 @@ SIGNATURES = {
     "mhe_assemble": (ctypes.c_int, [_P, c_vp, c_i32, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp,
                                     c_vp, c_vp, c_vp, c_vp]),
     "mhe_chol_solve": (ctypes.c_int, [_P, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "mhe_assemble_ws": (ctypes.c_int, [_P, c_vp, c_i32, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp,
+                                       c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
+    "mhe_chol_solve_ws": (ctypes.c_int, [_P, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "mhe_ekf_run": (ctypes.c_int, [_PE, c_i32, c_i32, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64,
                                    c_vp, c_i64, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "mhe_ls_run": (ctypes.c_int, [_PL, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,

@@ -393,22 +393,33 @@ class BatchSolver:
             keep_alive(s, cur, X, U_t, Y_t, PAR_t, W, F, E, Hm)
         return W, F, E, Hm
 
-    def assemble(self, X, U, Y, PAR=None, x0=None, stream=None):
-        """GN normal equations at X: H (B,dp,dp), g (B,dp), cost (B)."""
+    def assemble(self, X, U, Y, PAR=None, x0=None, stream=None, status_out=False):
+        """GN normal equations at X: H (B,dp,dp), g (B,dp), cost (B) -- dense, node-major
+        (row j*n + c; padding nodes last) on both paths.  The large-system path runs the
+        solve's own k_big_resid + k_big_assemble over a workspace (mhe_assemble_ws) and
+        copies H out of their component-major tiles.  ``status_out``: also return the
+        per-trajectory status (0, or 4 = constants built for other dims)."""
         self._check_ready()
         with launch_stream(stream, self.device, (self._built,)) as (s, cur):
             X, B, U_t, ustr, Y_t, PAR_t, pstr, x0_t = self._inputs(X, U, Y, PAR, x0)
             H = torch.empty((B, self.dp, self.dp), dtype=torch.float64, device=self.device)
             g = torch.empty((B, self.dp), dtype=torch.float64, device=self.device)
             cost = torch.empty(B, dtype=torch.float64, device=self.device)
-            rc = self.lib.mhe_assemble(self.dims, _ptr(self.cbuf), B, _ptr(X), _ptr(U_t), ustr, _ptr(Y_t),
-                                       _ptr(PAR_t), pstr, _ptr(x0_t), _ptr(H), _ptr(g), _ptr(cost), _handle(s))
-            _lib.check(rc, "mhe_assemble")
-            keep_alive(s, cur, X, U_t, Y_t, PAR_t, x0_t, H, g, cost)
+            status = torch.empty(B, dtype=torch.int32, device=self.device)
+            ws, nb = self._workspace(B, s)
+            rc = self.lib.mhe_assemble_ws(self.dims, _ptr(self.cbuf), B, _ptr(X), _ptr(U_t), ustr, _ptr(Y_t),
+                                          _ptr(PAR_t), pstr, _ptr(x0_t), _ptr(H), _ptr(g), _ptr(cost), _ptr(status),
+                                          _ptr(ws), nb, _handle(s))
+            _lib.check(rc, "mhe_assemble_ws")
+            keep_alive(s, cur, X, U_t, Y_t, PAR_t, x0_t, H, g, cost, status, ws)
+        if status_out:
+            return H, g, cost, status
         return H, g, cost
 
     def chol_solve(self, H, g, stream=None):
-        """delta = -H^{-1} g with the solver's tiled Cholesky (H: (B,dp,dp) SPD)."""
+        """delta = -H^{-1} g with the solver's own factorization (H: (B,dp,dp) SPD,
+        node-major as ``assemble`` returns it; lower triangle read): the register-tiled
+        kernel, or on the large-system path k_big_chol over a workspace (mhe_chol_solve_ws)."""
         self._check_ready()
         with launch_stream(stream, self.device, (self._built,)) as (s, cur):
             H = _dev(H, self.device)
@@ -418,10 +429,11 @@ class BatchSolver:
                 raise ValueError(f"H must be (B,{self.dp},{self.dp}) and g (B,{self.dp})")
             delta = torch.empty((B, self.dp), dtype=torch.float64, device=self.device)
             status = torch.empty(B, dtype=torch.int32, device=self.device)
-            rc = self.lib.mhe_chol_solve(self.dims, _ptr(self.cbuf), B, _ptr(H), _ptr(g), _ptr(delta),
-                                         _ptr(status), _handle(s))
-            _lib.check(rc, "mhe_chol_solve")
-            keep_alive(s, cur, H, g, delta, status)
+            ws, nb = self._workspace(B, s)
+            rc = self.lib.mhe_chol_solve_ws(self.dims, _ptr(self.cbuf), B, _ptr(H), _ptr(g), _ptr(delta),
+                                            _ptr(status), _ptr(ws), nb, _handle(s))
+            _lib.check(rc, "mhe_chol_solve_ws")
+            keep_alive(s, cur, H, g, delta, status, ws)
         return delta, status
 
 

@@ -221,3 +221,40 @@ def test_c4_configured_batch_strided_subset_matches_oracle():
     X, cost, iters, status = _np(s.solve(w.X_init, w.U, w.Y, w.PAR, max_iter=2, tol=0.0))
     idx = np.array([0, 511, 1023])
     _subset_vs_oracle(w, X, cost, iters, status, idx, 2, "C4 B=1024")
+
+
+def test_c5_configured_shard_chunked():
+    """C5 at its configured per-GPU shard (B = 2048, d = 8040: 0.52 GB of workspace per
+    trajectory, so the batch is streamed through one workspace in chunks of whole
+    CU-fulls, BatchSolver._chunk), 1 and 2 GN iterations.
+      * every trajectory runs the same iterations with the same status;
+      * trajectories at the ends, the middle and both sides of every chunk boundary equal
+        the same trajectories solved alone in one small launch, bitwise (a batch- or
+        chunk-offset bug shows here first);
+      * the first step of trajectories 0 and 2047 solves the ORACLE's normal equations at
+        X_init (tests/big_oracle.c5_normal_epochs, pinned to the dense oracle at N = 10):
+        normwise backward error of delta = X1 - X0 <= 1e-12 (the assembly tolerance of
+        tests/test_gpu_big_parity.py) + 8 eps max|X1| / max|delta| (X1 - X0 rounding) --
+        independent of cond(H).  Reference problem: gnss-multi-receiver.py:141-243."""
+    from big_oracle import backward_error, c5_normal_epochs, c5_problem
+    w = configs.make_c5(B=2048)
+    s = solver.from_workload(w)
+    chunk = s._chunk(w.B)
+    print(f"C5 B=2048: chunk {chunk}")
+    X1, c1, i1, st1 = _np(s.solve(w.X_init, w.U, w.Y, w.PAR, max_iter=1, tol=0.0))
+    X2, c2, i2, st2 = _np(s.solve(w.X_init, w.U, w.Y, w.PAR, max_iter=2, tol=0.0))
+    assert i1.tolist() == [1] * w.B and i2.tolist() == [2] * w.B
+    assert st1.tolist() == [solver.STATUS_MAX_ITER] * w.B and st2.tolist() == [solver.STATUS_MAX_ITER] * w.B
+    assert np.all(np.isfinite(X2)) and np.all(np.isfinite(c2))
+    edges = [e for k in range(chunk, w.B, chunk) for e in (k - 1, k)]
+    idx = np.unique(np.r_[0, w.B // 2 - 1, w.B - 1, edges]).astype(np.int64)
+    sub = s.solve(w.X_init[idx], w.U[idx], w.Y[idx], w.PAR, max_iter=2, tol=0.0)
+    Xs, cs, _, _ = _np(sub)
+    assert np.array_equal(Xs, X2[idx]) and np.array_equal(cs, c2[idx]), idx
+    pb = c5_problem(w)
+    for b in (0, w.B - 1):
+        H, g, _ = c5_normal_epochs(pb, w.X_init[b:b + 1], w.U[b:b + 1], w.Y[b:b + 1], w.PAR)
+        delta = (X1[b] - w.X_init[b]).ravel()
+        eta = backward_error(H[0], g[0], delta)
+        bnd = 1e-12 + 8 * np.finfo(np.float64).eps * np.abs(X1[b]).max() / np.abs(delta).max()
+        tl.check(f"C5 B=2048 trajectory {b}: first step vs oracle H, g (backward error)", eta, bnd)
