@@ -2053,16 +2053,20 @@ struct PairOps {
   int (*big_stage)(const mhe_dims* dm, BigArgs& A, int batch, int stage, hipStream_t st);
 };
 
-// compute units of the current device (cached per device)
-inline int device_cus() {
+// compute units of the device the launch stream belongs to (not the calling thread's
+// current device), cached per device; concurrent callers may both fill a slot, with
+// the same value (relaxed atomics: no torn or racy plain accesses)
+inline int device_cus(hipStream_t st) {
   static int cus[64] = {0};
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-  if (cus[dev] == 0) {
+  if (hipStreamGetDevice(st, &dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  int c = __atomic_load_n(&cus[dev], __ATOMIC_RELAXED);
+  if (c == 0) {
     int v = 0;
-    cus[dev] = hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0 ? v : 256;
+    c = hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0 ? v : 256;
+    __atomic_store_n(&cus[dev], c, __ATOMIC_RELAXED);
   }
-  return cus[dev];
+  return c;
 }
 
 template <class DYN, class MEAS>
@@ -2080,7 +2084,7 @@ int launch_gn(const mhe_dims* dm, GnArgs& a, int batch, int mode, hipStream_t st
       // a batch that gives each CU at most one trajectory runs the instance without the
       // two-workgroups-per-CU register cap (C2 strong scaling at 4-8 GPUs: 256 / 128 per GPU)
       kern = huber ? k_gn<DYN, MEAS, MAX_SLOTS, MODE_SOLVE, true>
-             : batch <= device_cus() ? k_gn<DYN, MEAS, MAX_SLOTS, MODE_SOLVE, false, 2>
+             : batch <= device_cus(st) ? k_gn<DYN, MEAS, MAX_SLOTS, MODE_SOLVE, false, 2>
                                      : k_gn<DYN, MEAS, MAX_SLOTS, MODE_SOLVE>;
     else if (mode == MODE_ASSEMBLE)
       kern = huber ? k_gn<DYN, MEAS, MAX_SLOTS, MODE_ASSEMBLE, true> : k_gn<DYN, MEAS, MAX_SLOTS, MODE_ASSEMBLE>;

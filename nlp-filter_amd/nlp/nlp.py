@@ -637,13 +637,11 @@ class fixedTimeOptimalEstimationNLP(NLP):
             g0 = gvals()
             for x, v in zip(self._X, saved):
                 x.value = v
-        start_active = [i for i in np.argsort(-g0) if g0[i] > 0]
-        if len(start_active) > 48 - n_fixed:
-            # the device's bordered step holds at most 48 rows (equality rows + extra
-            # variables + active inequality rows): refuse before any solve, not midway
-            raise UnsupportedFeature(f"{len(start_active)} inequality rows (bounds next to constraint rows count one "
-                                     f"per node) are violated at the start; at most {48 - n_fixed} can be held "
-                                     f"active beside {n_fixed} equality rows and extra variables")
+        # the device's bordered step holds at most 48 rows (equality rows + extra variables
+        # + active inequality rows): start with the most-violated rows up to that cap --
+        # holding them may pull the rest feasible; rows still violated once no room is
+        # left end the loop below with UnsupportedFeature
+        start_active = [i for i in np.argsort(-g0) if g0[i] > 0][:48 - n_fixed]
         self._active = start_active
         history = []
         for step in range(self.MAX_ACTIVE_SET_STEPS):

@@ -60,11 +60,11 @@ def load_reference_nlp():
     ref.measurements = g0._load("refobj_measurements", f"{REF}/nlp/measurements.py")
     ref.cost_functions = g0._load("refobj_cost_functions", f"{REF}/nlp/cost_functions.py")
     sys.path.insert(0, f"{REF}/utils")
+    saved = {k: sys.modules.get(k) for k in ("gnss", "utils")}  # before any load that may fail
     try:
         ref.gutils = g0._load("refobj_gutils", f"{REF}/utils/utils.py")
         ref.data = g0._load("refobj_data", f"{REF}/utils/data.py")
         ref.gnss = g0._load("refobj_gnss", f"{REF}/utils/gnss.py")
-        saved = {k: sys.modules.get(k) for k in ("gnss", "utils")}
         sys.modules["gnss"], sys.modules["utils"] = ref.gnss, ref.gutils   # leastsquares.py's flat imports
         ref.ls = g0._load("refobj_leastsquares", f"{REF}/utils/leastsquares.py")
         ref.vehicle_sim = g0._load("refobj_vehicle_sim", f"{REF}/utils/vehicle_sim.py")

@@ -1,8 +1,8 @@
 #!/bin/bash
 # A/B timing of two builds of the fused kernel on one box (run on the GPU box):
 #   tools/ab.sh "<libA.so> <libB.so> ..." [rounds] [batch] [log]   -> gpurun_out/<log> (default ab.log)
-# Alternates bench.py --no-cpu runs between the libraries (MHE_LIB); an entry
-# "<lib.so>@<waves>" also sets MHE_GN_WAVES (8 or 16: the fused kernel's shape).
+# Alternates bench.py --no-cpu runs between the libraries (MHE_LIB).  Kernel shapes are
+# build-time choices: build each variant as its own library (tools/build_from.sh).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 LIBS=$1; N=${2:-3}; BATCH=${3:-1024}
@@ -10,8 +10,7 @@ O=gpurun_out/${4:-ab.log}
 : > $O
 for i in $(seq $N); do
   for L in $LIBS; do
-    W=8; [[ $L == *@* ]] && W=${L#*@}
-    v=$(MHE_LIB=${L%@*} MHE_GN_WAVES=$W timeout -k 10 120 python bench.py --no-cpu --steps 30 --global-batch $BATCH 2>/dev/null | python -c "import sys,json; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); print(d['value'], d['roofline']['kernel_ms'])") || exit 1
+    v=$(MHE_LIB=$L timeout -k 10 120 python bench.py --no-cpu --steps 30 --global-batch $BATCH 2>/dev/null | python -c "import sys,json; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); print(d['value'], d['roofline']['kernel_ms'])") || exit 1
     echo "$L $v" >> $O
   done
 done
