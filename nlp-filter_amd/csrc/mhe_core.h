@@ -97,7 +97,7 @@ __host__ __device__ inline ConstLayout const_layout(int P, int M, int n, int p, 
 }
 
 struct SmemLayout {  // offsets in doubles
-  int Xs, Vs, FtV, Es, FtE, GE, G, LAM, BV, YV, PB, DT, RED, ROWM, UN, XO, ACT, GV, total;
+  int Xs, Vs, FtV, Es, FtE, GE, G, LAM, BV, YV, PB, HB, BAND, ZT, DT, RED, ROWM, UN, XO, ACT, GV, total;
 };
 
 __host__ __device__ inline int rnd2(int x) { return (x + 1) & ~1; }  // keep 16-B alignment
@@ -111,7 +111,10 @@ constexpr int UNITS = 68;
 constexpr int MFMA_NEG_A = 1;
 __host__ __device__ constexpr int unit_row(int i) { return (i & 1) ? 51 - i : 16 - i; }
 
-__host__ __device__ inline SmemLayout smem_layout(int P, int M, int n, int NT, bool nonlinear, bool bounded = false) {
+// sb: the small-batch factorization (factor_forward_sb): U block rows double-buffered
+// (PB) and the hand-off tile of the critical-path wave (HB, double-buffered)
+__host__ __device__ inline SmemLayout smem_layout(int P, int M, int n, int NT, bool nonlinear, bool bounded = false,
+                                                  bool sb = false) {
   SmemLayout S;
   int o = 0;
   const int dp = 16 * NT;
@@ -125,7 +128,10 @@ __host__ __device__ inline SmemLayout smem_layout(int P, int M, int n, int NT, b
   S.LAM = o;  o += rnd2(P * n);         // Huber IRLS weights c_k lambda_ka (MHE_COST_HUBER)
   S.BV = o;   o += dp;                  // right-hand side b = -g, updated block by block
   S.YV = o;   o += dp;                  // y = U^-T b, then delta = U^-1 y in place
-  S.PB = o;   o += (NT - 1) * 256;      // block row k of U (tiles U_kb, b > k), register order
+  S.PB = o;   o += (sb ? 2 : 1) * (NT - 1) * 256;  // block row k of U (tiles U_kb, b > k), register order
+  S.HB = o;   o += sb ? 2 * 256 : 0;
+  S.BAND = o; o += sb ? (NT - 1) * 256 : 0;  // the band tiles U_{k,k+1} (backward_sb reads them here)
+  S.ZT = o;   o += sb ? 256 : 0;             // a zero tile: operand loads of idle slots
   S.DT = o;   o += NT * DTS;            // diagonal blocks
   S.RED = o;  o += 4 * NW + 8;
   S.ROWM = o; o += NW * 8;              // per wave, per block row I: bit mask of its slots (I, J)
@@ -346,10 +352,11 @@ __device__ __forceinline__ void init_units(double* un) {
     for (int e = threadIdx.x; e < UNITS; e += 64) un[e] = (e == 16 || e == 51) ? 1.0 : 0.0;
 }
 
+template <int SLOTS = MAX_SLOTS>
 __device__ __forceinline__ void init_rowmask(int* rowm, int wave, int lane, int stab) {
   unsigned m = 0;
 #pragma unroll
-  for (int s = 0; s < MAX_SLOTS; ++s) {
+  for (int s = 0; s < SLOTS; ++s) {
     const int IJ = slot_ij(stab, s);
     if (IJ >= 0 && (IJ & 0xffff) == lane) m |= 1u << s;
   }
@@ -1339,6 +1346,226 @@ __device__ __forceinline__ bool factor_forward(const GnArgs& a, const SmemLayout
   return flag[0] == 0;
 }
 
+// ------------------------------------------------------------ small-batch factorization
+// When the batch gives each CU at most one trajectory (C2 strong scaling at 4 and 8
+// GPUs: 256 / 128 per GPU) a trajectory's GN iteration is a latency chain, and in the
+// factorization above every block step costs panel + two workgroup barriers + the T
+// and diagonal-update MFMAs of the next critical tile, one after another.
+// factor_forward_sb takes the critical chain P(k) -> T(k, k+1) -> D_{k+1} -> P(k+1) off
+// the workgroup barriers: ONE wave (CP, wave 0) runs it alone, one barrier per block
+// step, while six worker waves own the 78 off-diagonal tiles (13 slots each: the
+// one-workgroup-per-CU instance may use 256 VGPRs) and CP's SIMD partner (wave 4; waves
+// w and w + 4 share a SIMD) does only the forward substitution, so no MFMA of theirs
+// competes with the panel for that SIMD.  Interval k (between barriers k and k + 1):
+//   CP       A_{k,k+1} (handed over by its owner, updated through step k - 2)
+//              -= U_{k-1,k}^T U_{k-1,k+1};  U_{k,k+1} = L_kk^-1 A_{k,k+1} -> PB_k;
+//            D_{k+1} -= U_{k,k+1}^T U_{k,k+1};  panel(k + 1)
+//   workers  every owned tile (J, I), J >= k, other than (k, k+1): the deferred trailing
+//            update of step k - 1, A_JI -= U_{k-1,J}^T U_{k-1,I} (from PB_{k-1});
+//            row k tiles then T(k) -> PB_k and D_I -= U_kI^T U_kI (their own D_I);
+//            tile (k+1, k+2) is handed to CP (HB); CP keeps the band tiles U_{k,k+1} in
+//            LDS (BAND), where backward_sb reads them (their owners' registers go stale)
+//   wave 4   y_{k-1} = L^-1 b_{k-1}, b_b -= U_{k-1,b}^T y_{k-1}  (b >= k)
+// PB (rows k - 1 and k of U) and HB are double-buffered, so one barrier per interval
+// orders every hand-off.  Bitwise-identical per trajectory whatever the batch position;
+// not bitwise equal to factor_forward (other summation order of the trailing updates).
+constexpr int SB_WORKERS = 6;
+constexpr int SB_SLOTS = (MAX_NT * (MAX_NT - 1) / 2 + SB_WORKERS - 1) / SB_WORKERS;  // 13
+
+__device__ __forceinline__ int sb_worker(int wave) { return (wave == 0 || wave == 4) ? -1 : wave < 4 ? wave - 1 : wave - 2; }
+
+// slot table of factor_forward_sb: u = worker + 6 s over the tiles I > J, column-major
+__device__ __forceinline__ int make_slot_table_sb(int wave, int lane, int NT) {
+  const int w = sb_worker(wave);
+  const int u = w + SB_WORKERS * lane;
+  if (w < 0 || lane >= SB_SLOTS || u >= NT * (NT - 1) / 2) return -1;
+  int J = 0, base = 0;
+  while (u >= base + (NT - 1 - J)) {
+    base += NT - 1 - J;
+    ++J;
+  }
+  return (J + 1 + (u - base)) | (J << 16);
+}
+
+template <int SLOTS>
+__device__ __forceinline__ bool factor_forward_sb(const GnArgs& a, const SmemLayout& SL, double* sm,
+                                                  d4 (&acc)[SLOTS], int wave, int lane, int stab, DIAG_FDECL) {
+  double* BV = sm + SL.BV;
+  double* YV = sm + SL.YV;
+  double* DT = sm + SL.DT;
+  double* PB0 = sm + SL.PB;
+  double* HB0 = sm + SL.HB;
+  int* flag = (int*)(sm + SL.RED + 4 * NW);
+  const int NT = a.NT;
+  const int PBS = (NT - 1) * 256;
+  bool bad = false;
+  // prologue: panel(0) on CP; the owner of tile (0, 1) hands it over
+  if (wave == 0) {
+    __builtin_amdgcn_s_setprio(3);
+    bad |= panel(DT, sm + SL.UN, lane);
+    __builtin_amdgcn_s_setprio(0);
+  } else {
+#pragma unroll
+    for (int s = 0; s < SLOTS; ++s)
+      if (slot_ij(stab, s) == 1)  // tile (I, J) = (1, 0)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) HB0[r * 64 + lane] = acc[s][r];
+  }
+  __syncthreads();
+#pragma unroll 1
+  for (int k = 0; k < NT; ++k) {
+    int lane_o = lane, stab_o = stab;
+    asm volatile("" : "+v"(lane_o));
+    asm volatile("" : "+v"(stab_o));
+    const double* PBp = PB0 + ((k + 1) & 1) * PBS;  // U block row k - 1
+    double* PBk = PB0 + (k & 1) * PBS;              // U block row k
+    if (wave == 0) {
+      if (k + 1 < NT) {
+        __builtin_amdgcn_s_setprio(3);
+        const double* hb = HB0 + (k & 1) * 256;
+        d4 t;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) t[r] = hb[r * 64 + lane_o];
+        if (k >= 1) {
+          double av[4], bv[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            av[r] = PBp[r * 64 + lane_o];        // U_{k-1,k}
+            bv[r] = PBp[256 + r * 64 + lane_o];  // U_{k-1,k+1}
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) t = __builtin_amdgcn_mfma_f64_16x16x4f64(av[r], bv[r], t, 0, 0, 0);
+        }
+        const double* LT = DT + k * DTS;
+        double la[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) la[r] = LT[(4 * r + (lane_o >> 4)) * LIS + (lane_o & 15)];
+        double* DTn = DT + (k + 1) * DTS;
+        d4 dn;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dn[r] = DTn[r * 64 + lane_o];
+        d4 u = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) u = __builtin_amdgcn_mfma_f64_16x16x4f64(la[r], t[r], u, 0, 0, MFMA_NEG_A);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dn = __builtin_amdgcn_mfma_f64_16x16x4f64(u[r], u[r], dn, 0, 0, MFMA_NEG_A);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          PBk[r * 64 + lane_o] = u[r];
+          DTn[r * 64 + lane_o] = dn[r];
+          sm[SL.BAND + k * 256 + r * 64 + lane_o] = u[r];
+        }
+        wave_lds_sync();
+        DIAG_MARK(8);
+        if (!KO(3)) bad |= panel(DTn, sm + SL.UN, lane_o);
+        __builtin_amdgcn_s_setprio(0);
+        DIAG_MARK(12);
+      }
+    } else if (wave == 4) {
+      if (k >= 1) {
+        block_fwd(DT + (k - 1) * DTS, BV + 16 * (k - 1), YV + 16 * (k - 1), lane_o);
+        wave_lds_sync();
+        for (int v = lane_o; v < 16 * (NT - k); v += 64) {
+          const int bq = k + (v >> 4), c = v & 15;
+          const double* ub = PBp + (bq - k) * 256 + c;
+          double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+          for (int q = 0; q < 16; q += 2) {
+            s0 += ub[q * 16] * YV[16 * (k - 1) + q];
+            s1 += ub[(q + 1) * 16] * YV[16 * (k - 1) + q + 1];
+          }
+          BV[16 * bq + c] -= s0 + s1;
+        }
+      }
+    }
+    {
+      // the workers' slot work, outside the role branches (CP and wave 4 own no slots:
+      // their masks are 0), so the accumulators are only ever modified under per-slot
+      // bits -- a role branch around them made the compiler keep a second copy of all
+      // 13 slots and copy it back every interval.  Roles of this interval's slots
+      // (worker w owns tiles u = w + 6 s, column-major; row J starts at u = base(J)):
+      //   mA  tiles of rows >= k but the band tile (k, k+1): deferred update of step k-1
+      //   mT  row k but the band tile: T(k) and D_I
+      //   mH  tile (k+1, k+2): handed to CP
+      const int w = sb_worker(wave);
+      unsigned mA = 0, mT = 0, mH = 0;
+      if (w >= 0) {
+        const int ntl = NT * (NT - 1) / 2;
+        auto base = [NT](int J) { return J * (NT - 1) - J * (J - 1) / 2; };
+        auto cdiv = [](int x) { return x <= 0 ? 0 : (x + SB_WORKERS - 1) / SB_WORKERS; };
+        auto range = [](int lo, int hi) { return lo < hi ? (1u << hi) - (1u << lo) : 0u; };
+        const int b0 = k < NT ? base(k) : ntl, b1 = k + 1 < NT ? base(k + 1) : ntl;
+        if (k >= 1) mA = range(cdiv(b0 - w), cdiv(ntl - w));
+        if (k + 1 < NT && b0 % SB_WORKERS == w) mA &= ~(1u << (b0 / SB_WORKERS));
+        mT = range(cdiv(b0 + 1 - w), cdiv(b1 - w));
+        if (k + 2 < NT && b1 % SB_WORKERS == w) mH = 1u << (b1 / SB_WORKERS);
+      }
+      if (w >= 0) {
+      const double* LT = DT + k * DTS;
+      double la[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) la[r] = LT[(4 * r + (lane_o >> 4)) * LIS + (lane_o & 15)];
+      // three passes (the deferred updates, then T, then the hand-off) rather than one
+      // per slot: every update accumulates into its slot in place; a slot that T
+      // rewrites in the same pass as its update made the compiler keep the whole
+      // accumulator array in temporaries and copy it back every interval
+#pragma unroll
+      for (int s = 0; s < SLOTS; ++s) {
+        if (((mA >> s) & 1u) && !KO(1)) {
+          const int IJ = slot_ij(stab_o, s);
+          const double* ua = PBp + ((IJ >> 16) - k) * 256 + lane_o;
+          const double* ub = PBp + ((IJ & 0xffff) - k) * 256 + lane_o;
+          double av[4], bv[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            av[r] = ua[64 * r];
+            bv[r] = ub[64 * r];
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[r], bv[r], acc[s], 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < SLOTS; ++s) {
+        if ((mT >> s) & 1u) {
+          const int I = slot_ij(stab_o, s) & 0xffff;
+          d4 u = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+          for (int r = 0; r < 4; ++r) u = __builtin_amdgcn_mfma_f64_16x16x4f64(la[r], acc[s][r], u, 0, 0, MFMA_NEG_A);
+          if (!KO(0)) acc[s] = u;
+          double* DTi = DT + I * DTS;
+          d4 di;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            PBk[(I - k - 1) * 256 + r * 64 + lane_o] = u[r];
+            di[r] = DTi[r * 64 + lane_o];
+          }
+          if (!KO(2)) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) di = __builtin_amdgcn_mfma_f64_16x16x4f64(u[r], u[r], di, 0, 0, MFMA_NEG_A);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) DTi[r * 64 + lane_o] = di[r];
+          }
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < SLOTS; ++s) {
+        if ((mH >> s) & 1u) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) HB0[((k + 1) & 1) * 256 + r * 64 + lane_o] = acc[s][r];
+        }
+      }
+      }
+    }
+    DIAG_MARK(13);
+    __syncthreads();
+    DIAG_MARK(11);
+  }
+  if (bad && lane == 0) flag[0] = 1;  // flag was zeroed at kernel start
+  __syncthreads();
+  return flag[0] == 0;
+}
+
 // Sum over the four 16-lane rows of a wave (v_permlane16/32_swap), result in every row.
 __device__ __forceinline__ double rows4_sum(double v) {
   long long b = __double_as_longlong(v);
@@ -1451,6 +1678,60 @@ __device__ __forceinline__ void backward(const GnArgs& a, const SmemLayout& SL, 
   }
 }
 
+// backward() for factor_forward_sb: the critical tile of every block step is the band
+// tile U_{bb-1,bb}, which CP kept in LDS (BAND) -- CP (wave 0, no tiles of its own)
+// forms delta_{bb-1} from it while the workers subtract their tiles (J, bb), J < bb - 1,
+// from y_J out of their registers.  Same operations and order per element as backward().
+template <int SLOTS>
+__device__ __forceinline__ void backward_sb(const GnArgs& a, const SmemLayout& SL, double* sm,
+                                            d4 (&acc)[SLOTS], int wave, int lane, int stab) {
+  const double* DT = sm + SL.DT;
+  double* DV = sm + SL.YV;
+  const int NT = a.NT;
+  if (wave == 0) {
+    const double* BV = sm + SL.BV;
+    block_fwd(DT + (NT - 1) * DTS, BV + 16 * (NT - 1), DV + 16 * (NT - 1), lane);  // y_{NT-1}
+    wave_lds_sync();
+    block_back(DT + (NT - 1) * DTS, DV + 16 * (NT - 1), lane);
+  }
+  __syncthreads();
+#pragma unroll 1
+  for (int bb = NT - 1; bb >= 1 && !KO(5); --bb) {
+    int lane_o = lane, stab_o = stab;
+    asm volatile("" : "+v"(lane_o));
+    asm volatile("" : "+v"(stab_o));
+    const double db = DV[16 * bb + (lane_o & 15)];
+    const int g = lane_o >> 4, c = lane_o & 15;
+    if (wave == 0) {
+      const int J = bb - 1;
+      const double* ut = sm + SL.BAND + J * 256 + lane_o;
+      double* yj = DV + 16 * J;
+      double part[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) part[r] = row16_sum(ut[64 * r] * db);
+      const double* LT = DT + J * DTS;
+      double sd = 0.0;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sd += LT[c * LIS + g + 4 * r] * (yj[g + 4 * r] - part[r]);
+      const double dv = rows4_sum(sd);
+      if (lane_o < 16) yj[c] = dv;
+    } else if (!KO(6)) {
+      const unsigned rm = __builtin_amdgcn_readfirstlane(((const int*)(sm + SL.ROWM))[wave * 16 + bb]);
+#pragma unroll
+      for (int s = SLOTS - 1; s >= 0; --s) {
+        if (!((rm >> s) & 1u)) continue;
+        const int J = slot_ij(stab_o, s) >> 16;
+        if (J == bb - 1) continue;  // the band tile: CP's, from LDS
+        double* yj = DV + 16 * J;
+        const double v[4] = {acc[s][0] * db, acc[s][1] * db, acc[s][2] * db, acc[s][3] * db};
+        const double z = row16_sum4(v, c);
+        if ((c & 3) == 0) yj[g + 4 * (2 * (c >> 3) + ((c >> 2) & 1))] -= z;
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // The constants buffer starts with a 256-B header whose first word is a stamp of the
 // dims that define its layout (const_tag); a solve whose dims disagree computes
 // nothing and reports MHE_STATUS_BAD_CONSTANTS.  The stamp sits at offset 0, so the
@@ -1489,25 +1770,29 @@ __device__ __forceinline__ int opaque_s(int x) {
 }
 #define FA a
 #define FCL const_layout(opaque_s(a.P), opaque_s(a.M), n, MEAS::p, opaque_s(a.NT))
-#define FSL smem_layout(opaque_s(a.P), opaque_s(a.M), n, opaque_s(a.NT), !MEAS::LINEAR)
+#define FSL smem_layout(opaque_s(a.P), opaque_s(a.M), n, opaque_s(a.NT), !MEAS::LINEAR, false, SB)
 
 // MINW (launch bounds' 2nd argument): min waves per SIMD -- 4 = two workgroups (trajectories)
 // per CU, 128 VGPRs; 2 = the small-batch instance (batch <= CUs: one workgroup per CU
 // anyway), which may use 256 VGPRs
-template <class DYN, class MEAS, int SLOTS, int mode, bool HUBER = false, int MINW = MHE_GN_MINW>
+// SB: the small-batch factorization (factor_forward_sb, MODE_SOLVE with MINW = 2 only)
+template <class DYN, class MEAS, int SLOTS, int mode, bool HUBER = false, int MINW = MHE_GN_MINW, bool SB = false>
 __global__ __launch_bounds__(NTHREADS, MINW) void k_gn(GnArgs a) {
   constexpr int n = DYN::n;
+  static_assert(!SB || (mode == MODE_SOLVE && MINW <= 2 && NW == 8), "small-batch factorization: one workgroup per CU");
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const ConstLayout CL = const_layout(a.P, a.M, n, MEAS::p, a.NT);
-  const SmemLayout SL = smem_layout(a.P, a.M, n, a.NT, !MEAS::LINEAR);
+  const SmemLayout SL = smem_layout(a.P, a.M, n, a.NT, !MEAS::LINEAR, false, SB);
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int b = blockIdx.x;
-  const int stab = make_slot_table(wave, lane, a.NT);
-  init_rowmask((int*)(sm + SL.ROWM), wave, lane, stab);
+  const int stab = SB ? make_slot_table_sb(wave, lane, a.NT) : make_slot_table(wave, lane, a.NT);
+  init_rowmask<SLOTS>((int*)(sm + SL.ROWM), wave, lane, stab);
   double* Xs = sm + SL.Xs;
   if (threadIdx.x == 0) *(int*)(sm + SL.RED + 4 * NW) = 0;  // NOT_SPD flag
   init_units(sm + SL.UN);
+  if constexpr (SB)
+    for (int t = threadIdx.x; t < 256; t += NTHREADS) sm[SL.ZT + t] = 0.0;
   double* DV = sm + SL.YV;  // delta after backward()
   double* RED = sm + SL.RED;
   d4 acc[SLOTS];
@@ -1586,13 +1871,20 @@ __global__ __launch_bounds__(NTHREADS, MINW) void k_gn(GnArgs a) {
     DIAG_MARK(15);
     __syncthreads();
     DIAG_MARK(2);
-    const bool ok = factor_forward<SLOTS>(FA, FSL, sm, acc, wave, lane, stab, DIAG_FARGS);
+    bool ok;
+    if constexpr (SB)
+      ok = factor_forward_sb<SLOTS>(FA, FSL, sm, acc, wave, lane, stab, DIAG_FARGS);
+    else
+      ok = factor_forward<SLOTS>(FA, FSL, sm, acc, wave, lane, stab, DIAG_FARGS);
     DIAG_MARK(3);
     if (!ok) {
       status = MHE_STATUS_NOT_SPD;
       break;
     }
-    backward<SLOTS>(FA, FSL, sm, acc, wave, lane, stab);
+    if constexpr (SB)
+      backward_sb<SLOTS>(FA, FSL, sm, acc, wave, lane, stab);
+    else
+      backward<SLOTS>(FA, FSL, sm, acc, wave, lane, stab);
     DIAG_MARK(4);
     // X += delta (bounded problems run k_gn_bounded).  A non-finite delta is flagged
     // as an infinite step (NONFINITE, X untouched).
@@ -1922,11 +2214,11 @@ inline bool meas_info(int id, int n, int& p, int& q, bool& linear) {
 // the large-system path so both paths can be compared on identical inputs.
 // Mixed-row problems, extra variables and equality constraints
 // always take the large-system path (it carries the bordered KKT step).
-inline int smem_bytes(const mhe_dims* dm, int NT, bool bounded = false) {
+inline int smem_bytes(const mhe_dims* dm, int NT, bool bounded = false, bool sb = false) {
   int p, q;
   bool lin;
   meas_info(dm->meas_model, dm->n, p, q, lin);
-  return smem_layout(dm->N + 1, dm->M, dm->n, NT, !lin, bounded).total * (int)sizeof(double);
+  return smem_layout(dm->N + 1, dm->M, dm->n, NT, !lin, bounded, sb).total * (int)sizeof(double);
 }
 
 // The register-resident kernel keeps per-row measurement blocks G_i (n x n) in LDS;
@@ -2075,17 +2367,20 @@ int launch_gn(const mhe_dims* dm, GnArgs& a, int batch, int mode, hipStream_t st
     return MHE_ERR_UNSUPPORTED;  // mixed rows: large-system path only
   } else {
     const bool bounded = mode == MODE_SOLVE && dm->n_bounds > 0;
-    const int smem = smem_bytes(dm, a.NT, bounded) + g_opt_smem_pad;  // pad: mhe_set_option, occupancy A/B only
+    const bool huber = dm->dyn_cost == MHE_COST_HUBER;
+    // a batch that gives each CU at most one trajectory runs the small-batch instance:
+    // 256 VGPRs (no two-workgroups-per-CU register cap) and factor_forward_sb (C2 strong
+    // scaling at 4-8 GPUs: 256 / 128 per GPU)
+    const bool sb = mode == MODE_SOLVE && !bounded && !huber && batch <= device_cus(st) &&
+                    smem_bytes(dm, a.NT, false, true) + g_opt_smem_pad <= REG_LDS_LIMIT;
+    const int smem = smem_bytes(dm, a.NT, bounded, sb) + g_opt_smem_pad;  // pad: mhe_set_option, occupancy A/B only
     if (smem > REG_LDS_LIMIT) return MHE_ERR_UNSUPPORTED;
     void (*kern)(GnArgs) = nullptr;
-    const bool huber = dm->dyn_cost == MHE_COST_HUBER;
     if (bounded) kern = huber ? k_gn_bounded<DYN, MEAS, MAX_SLOTS, true> : k_gn_bounded<DYN, MEAS, MAX_SLOTS>;
     else if (mode == MODE_SOLVE)
-      // a batch that gives each CU at most one trajectory runs the instance without the
-      // two-workgroups-per-CU register cap (C2 strong scaling at 4-8 GPUs: 256 / 128 per GPU)
       kern = huber ? k_gn<DYN, MEAS, MAX_SLOTS, MODE_SOLVE, true>
-             : batch <= device_cus(st) ? k_gn<DYN, MEAS, MAX_SLOTS, MODE_SOLVE, false, 2>
-                                     : k_gn<DYN, MEAS, MAX_SLOTS, MODE_SOLVE>;
+             : sb  ? k_gn<DYN, MEAS, SB_SLOTS, MODE_SOLVE, false, 2, true>
+                   : k_gn<DYN, MEAS, MAX_SLOTS, MODE_SOLVE>;
     else if (mode == MODE_ASSEMBLE)
       kern = huber ? k_gn<DYN, MEAS, MAX_SLOTS, MODE_ASSEMBLE, true> : k_gn<DYN, MEAS, MAX_SLOTS, MODE_ASSEMBLE>;
     else kern = k_gn<DYN, MEAS, MAX_SLOTS, MODE_LINSOLVE>;

@@ -1,9 +1,10 @@
 #!/bin/bash
 # A/B variant of libmhe.so from a copy of the sources with some files taken from a git
 # revision: tools/build_from.sh NAME REV "file1 file2 ..." ["-DFLAG ..."]
-#   -> tools/libmhe_NAME.so (e.g. the previous revision of one kernel header); never
+#   -> ab/libmhe_NAME.so (e.g. the previous revision of one kernel header); never
 #   loaded by the product.
 set -e
+mkdir -p "$(cd "$(dirname "$0")/.." && pwd)/ab"
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 NAME=$1; REV=$2; FILES=$3; VFLAGS=$4
 S=/tmp/mhe_src_$NAME
@@ -16,4 +17,4 @@ for s in mhe_gn pair_vdp pair_integrators pair_gnss pair_vehicles pair_receivers
   /opt/rocm/bin/hipcc $FLAGS -c -o $S/$s.o $S/csrc/$s.hip &
 done
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $ROOT/tools/libmhe_$NAME.so $S/*.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $ROOT/ab/libmhe_$NAME.so $S/*.o

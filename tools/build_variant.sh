@@ -1,7 +1,8 @@
 #!/bin/bash
 # Full A/B variant of libmhe.so (all plug-in pairs): tools/build_variant.sh NAME "-DFLAG=1 ..."
-# -> tools/libmhe_NAME.so (objects in /tmp/mhe_variant_NAME); never loaded by the product.
+# -> ab/libmhe_NAME.so (objects in /tmp/mhe_variant_NAME); never loaded by the product.
 set -e
+mkdir -p "$(cd "$(dirname "$0")/.." && pwd)/ab"
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 NAME=$1; VFLAGS=$2
 B=/tmp/mhe_variant_$NAME
@@ -11,4 +12,4 @@ for s in mhe_gn pair_vdp pair_integrators pair_gnss pair_vehicles pair_receivers
   /opt/rocm/bin/hipcc $FLAGS -c -o $B/$s.o $ROOT/nlp-filter_amd/csrc/$s.hip &
 done
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $ROOT/tools/libmhe_$NAME.so $B/*.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $ROOT/ab/libmhe_$NAME.so $B/*.o
