@@ -1369,16 +1369,34 @@ __device__ __forceinline__ bool factor_forward(const GnArgs& a, const SmemLayout
 // PB (rows k - 1 and k of U) and HB are double-buffered, so one barrier per interval
 // orders every hand-off.  Bitwise-identical per trajectory whatever the batch position;
 // not bitwise equal to factor_forward (other summation order of the trailing updates).
+#ifndef MHE_SB_WEIGHTED
+#define MHE_SB_WEIGHTED 0  // A/B: 7:6 weighted tile shares (factorization -10 %, build / backward slower: -3 % overall)
+#endif
 constexpr int SB_WORKERS = 6;
-constexpr int SB_SLOTS = (MAX_NT * (MAX_NT - 1) / 2 + SB_WORKERS - 1) / SB_WORKERS;  // 13
+// Waves w and w + 4 share a SIMD, and the older one (1, 2, 3) wins the issue arbitration
+// of every pair, so with equal shares the younger one (5, 6, 7) finished an interval
+// ~20 % later.  The tiles are dealt by smooth weighted round robin, weights 7 : 6 for the
+// older / younger workers (0-2 = waves 1-3, 3-5 = waves 5-7): 14 and 12 tiles, and every
+// interval's active tiles split about 7 : 6 as well.
+constexpr int SB_SLOTS = MHE_SB_WEIGHTED ? 14 : (MAX_NT * (MAX_NT - 1) / 2 + SB_WORKERS - 1) / SB_WORKERS;
+__constant__ const unsigned char SB_OWNER[MAX_NT * (MAX_NT - 1) / 2] = {
+    0, 1, 2, 3, 4, 5, 0, 1, 2, 3, 4, 5, 0, 1, 2, 3, 4, 5, 0, 1, 2, 3, 4, 5, 0, 1, 2, 3, 4, 5, 0, 1, 2, 3, 4, 5, 0, 1, 2,
+    0, 1, 2, 3, 4, 5, 0, 1, 2, 3, 4, 5, 0, 1, 2, 3, 4, 5, 0, 1, 2, 3, 4, 5, 0, 1, 2, 3, 4, 5, 0, 1, 2, 3, 4, 5, 0, 1, 2};
 
 __device__ __forceinline__ int sb_worker(int wave) { return (wave == 0 || wave == 4) ? -1 : wave < 4 ? wave - 1 : wave - 2; }
 
-// slot table of factor_forward_sb: u = worker + 6 s over the tiles I > J, column-major
+__device__ __forceinline__ int sb_owner(int u) { return MHE_SB_WEIGHTED ? SB_OWNER[u] : u % SB_WORKERS; }
+
+// slot table of factor_forward_sb: the s-th tile (column-major over I > J) that this
+// wave's worker owns
 __device__ __forceinline__ int make_slot_table_sb(int wave, int lane, int NT) {
   const int w = sb_worker(wave);
-  const int u = w + SB_WORKERS * lane;
-  if (w < 0 || lane >= SB_SLOTS || u >= NT * (NT - 1) / 2) return -1;
+  if (w < 0 || lane >= SB_SLOTS) return -1;
+  const int ntl = NT * (NT - 1) / 2;
+  int u = 0, seen = 0;
+  for (; u < ntl; ++u)
+    if (sb_owner(u) == w && seen++ == lane) break;
+  if (u >= ntl) return -1;
   int J = 0, base = 0;
   while (u >= base + (NT - 1 - J)) {
     base += NT - 1 - J;
@@ -1387,9 +1405,33 @@ __device__ __forceinline__ int make_slot_table_sb(int wave, int lane, int NT) {
   return (J + 1 + (u - base)) | (J << 16);
 }
 
+// The slot masks of every interval of factor_forward_sb, lane k holding interval k's:
+// computed once per launch from the slot table (the GN loop then reads them with one
+// v_readlane each per interval).
+struct SbMasks {
+  unsigned A, T, H;
+};
+template <int SLOTS>
+__device__ __forceinline__ SbMasks sb_masks(int lane, int stab, int NT) {
+  SbMasks m = {0u, 0u, 0u};
+  const int k = lane;
+#pragma unroll
+  for (int s = 0; s < SLOTS; ++s) {
+    const int IJ = slot_ij(stab, s);
+    const int I = IJ & 0xffff, J = IJ >> 16;
+    const bool ok = IJ >= 0 && k < NT;
+    const bool band = J == k && I == k + 1;
+    m.A |= (ok && k >= 1 && J >= k && !band) ? 1u << s : 0u;  // deferred update of step k - 1
+    m.T |= (ok && J == k && !band) ? 1u << s : 0u;             // T(k) and D_I
+    m.H |= (ok && J == k + 1 && I == k + 2) ? 1u << s : 0u;    // next band tile to CP
+  }
+  return m;
+}
+
 template <int SLOTS>
 __device__ __forceinline__ bool factor_forward_sb(const GnArgs& a, const SmemLayout& SL, double* sm,
-                                                  d4 (&acc)[SLOTS], int wave, int lane, int stab, DIAG_FDECL) {
+                                                  d4 (&acc)[SLOTS], int wave, int lane, int stab, SbMasks mv,
+                                                  DIAG_FDECL) {
   double* BV = sm + SL.BV;
   double* YV = sm + SL.YV;
   double* DT = sm + SL.DT;
@@ -1412,6 +1454,11 @@ __device__ __forceinline__ bool factor_forward_sb(const GnArgs& a, const SmemLay
         for (int r = 0; r < 4; ++r) HB0[r * 64 + lane] = acc[s][r];
   }
   __syncthreads();
+#ifdef MHE_DIAG
+  // every wave's busy time per interval (diagnostic build only), in the ZT region
+  unsigned long long wt0 = __builtin_amdgcn_s_memtime();
+  unsigned long long* busy = (unsigned long long*)(sm + SL.ZT);  // [wave][k], k < 16
+#endif
 #pragma unroll 1
   for (int k = 0; k < NT; ++k) {
     int lane_o = lane, stab_o = stab;
@@ -1487,19 +1534,17 @@ __device__ __forceinline__ bool factor_forward_sb(const GnArgs& a, const SmemLay
       //   mA  tiles of rows >= k but the band tile (k, k+1): deferred update of step k-1
       //   mT  row k but the band tile: T(k) and D_I
       //   mH  tile (k+1, k+2): handed to CP
+#ifdef MHE_DIAG_SUB
+      unsigned long long st0 = __builtin_amdgcn_s_memtime();
+      if (wave == 1 && lane == 0 && k < 16) busy[7 * 16 + k] = st0 - wt0;
+#endif
       const int w = sb_worker(wave);
-      unsigned mA = 0, mT = 0, mH = 0;
-      if (w >= 0) {
-        const int ntl = NT * (NT - 1) / 2;
-        auto base = [NT](int J) { return J * (NT - 1) - J * (J - 1) / 2; };
-        auto cdiv = [](int x) { return x <= 0 ? 0 : (x + SB_WORKERS - 1) / SB_WORKERS; };
-        auto range = [](int lo, int hi) { return lo < hi ? (1u << hi) - (1u << lo) : 0u; };
-        const int b0 = k < NT ? base(k) : ntl, b1 = k + 1 < NT ? base(k + 1) : ntl;
-        if (k >= 1) mA = range(cdiv(b0 - w), cdiv(ntl - w));
-        if (k + 1 < NT && b0 % SB_WORKERS == w) mA &= ~(1u << (b0 / SB_WORKERS));
-        mT = range(cdiv(b0 + 1 - w), cdiv(b1 - w));
-        if (k + 2 < NT && b1 % SB_WORKERS == w) mH = 1u << (b1 / SB_WORKERS);
-      }
+      const unsigned mA = __builtin_amdgcn_readlane(mv.A, k), mT = __builtin_amdgcn_readlane(mv.T, k),
+                     mH = __builtin_amdgcn_readlane(mv.H, k);
+#ifdef MHE_DIAG_SUB
+      unsigned long long st1 = __builtin_amdgcn_s_memtime();
+      if (wave == 1 && lane == 0 && k < 16) busy[2 * 16 + k] = st1 - st0;
+#endif
       if (w >= 0) {
       const double* LT = DT + k * DTS;
       double la[4];
@@ -1509,22 +1554,30 @@ __device__ __forceinline__ bool factor_forward_sb(const GnArgs& a, const SmemLay
       // per slot: every update accumulates into its slot in place; a slot that T
       // rewrites in the same pass as its update made the compiler keep the whole
       // accumulator array in temporaries and copy it back every interval
+      auto upd_ops = [&](int s, double (&av)[4], double (&bv)[4]) {
+        const int IJ = slot_ij(stab_o, s);
+        const double* ua = PBp + ((IJ >> 16) - k) * 256 + lane_o;
+        const double* ub = PBp + ((IJ & 0xffff) - k) * 256 + lane_o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          av[r] = ua[64 * r];
+          bv[r] = ub[64 * r];
+        }
+      };
 #pragma unroll
       for (int s = 0; s < SLOTS; ++s) {
         if (((mA >> s) & 1u) && !KO(1)) {
-          const int IJ = slot_ij(stab_o, s);
-          const double* ua = PBp + ((IJ >> 16) - k) * 256 + lane_o;
-          const double* ub = PBp + ((IJ & 0xffff) - k) * 256 + lane_o;
           double av[4], bv[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            av[r] = ua[64 * r];
-            bv[r] = ub[64 * r];
-          }
+          upd_ops(s, av, bv);
 #pragma unroll
           for (int r = 0; r < 4; ++r) acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[r], bv[r], acc[s], 0, 0, 0);
         }
       }
+#ifdef MHE_DIAG_SUB
+      __builtin_amdgcn_s_waitcnt(0);
+      unsigned long long st2 = __builtin_amdgcn_s_memtime();
+      if (wave == 1 && lane == 0 && k < 16) busy[3 * 16 + k] = st2 - st1;
+#endif
 #pragma unroll
       for (int s = 0; s < SLOTS; ++s) {
         if ((mT >> s) & 1u) {
@@ -1548,6 +1601,11 @@ __device__ __forceinline__ bool factor_forward_sb(const GnArgs& a, const SmemLay
           }
         }
       }
+#ifdef MHE_DIAG_SUB
+      __builtin_amdgcn_s_waitcnt(0);
+      unsigned long long st3 = __builtin_amdgcn_s_memtime();
+      if (wave == 1 && lane == 0 && k < 16) busy[5 * 16 + k] = st3 - st2;
+#endif
 #pragma unroll
       for (int s = 0; s < SLOTS; ++s) {
         if ((mH >> s) & 1u) {
@@ -1558,9 +1616,39 @@ __device__ __forceinline__ bool factor_forward_sb(const GnArgs& a, const SmemLay
       }
     }
     DIAG_MARK(13);
+#ifdef MHE_DIAG
+#ifdef MHE_DIAG_SUB
+    if ((wave == 0 || wave == 1 || wave == 4) && lane == 0 && k < 16) busy[wave * 16 + k] = __builtin_amdgcn_s_memtime() - wt0;
+#else
+    if (lane == 0 && k < 16) busy[wave * 16 + k] = __builtin_amdgcn_s_memtime() - wt0;
+#endif
+#endif
     __syncthreads();
+#ifdef MHE_DIAG
+    wt0 = __builtin_amdgcn_s_memtime();
+#endif
     DIAG_MARK(11);
   }
+#ifdef MHE_DIAG
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    // 9: sum over intervals of the slowest worker's busy time; 10: of its excess over
+    // CP's; 13: wave 4's (forward substitution) busy time
+    for (int k = 0; k < NT && k < 16; ++k) {
+      unsigned long long mx = 0;
+      for (int w = 1; w < NW; ++w)
+        if (w != 4 && busy[w * 16 + k] > mx) mx = busy[w * 16 + k];
+      _dg[9] += mx;
+      _dg[10] += mx > busy[k] ? mx - busy[k] : 0;
+      _dg[13] += busy[4 * 16 + k];
+    }
+    if (blockIdx.x == 0 && a.dbg)  // block 0's matrix after the per-block stats (diag_phases.py)
+      for (int t = 0; t < 8 * 16; ++t) a.dbg[(size_t)gridDim.x * 16 + t] += busy[t];
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < 256; t += NTHREADS) sm[SL.ZT + t] = 0.0;  // the zero tile again
+  __syncthreads();
+#endif
   if (bad && lane == 0) flag[0] = 1;  // flag was zeroed at kernel start
   __syncthreads();
   return flag[0] == 0;
@@ -1788,6 +1876,8 @@ __global__ __launch_bounds__(NTHREADS, MINW) void k_gn(GnArgs a) {
   const int b = blockIdx.x;
   const int stab = SB ? make_slot_table_sb(wave, lane, a.NT) : make_slot_table(wave, lane, a.NT);
   init_rowmask<SLOTS>((int*)(sm + SL.ROWM), wave, lane, stab);
+  SbMasks sbm = {0u, 0u, 0u};
+  if constexpr (SB) sbm = sb_masks<SLOTS>(lane, stab, a.NT);
   double* Xs = sm + SL.Xs;
   if (threadIdx.x == 0) *(int*)(sm + SL.RED + 4 * NW) = 0;  // NOT_SPD flag
   init_units(sm + SL.UN);
@@ -1873,7 +1963,7 @@ __global__ __launch_bounds__(NTHREADS, MINW) void k_gn(GnArgs a) {
     DIAG_MARK(2);
     bool ok;
     if constexpr (SB)
-      ok = factor_forward_sb<SLOTS>(FA, FSL, sm, acc, wave, lane, stab, DIAG_FARGS);
+      ok = factor_forward_sb<SLOTS>(FA, FSL, sm, acc, wave, lane, stab, sbm, DIAG_FARGS);
     else
       ok = factor_forward<SLOTS>(FA, FSL, sm, acc, wave, lane, stab, DIAG_FARGS);
     DIAG_MARK(3);

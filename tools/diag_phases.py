@@ -20,7 +20,7 @@ B = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
 iters = int(sys.argv[2]) if len(sys.argv) > 2 else 4
 lib = _lib.load()
 lib.mhe_diag_set_buffer.argtypes = [ctypes.c_void_p]
-dbg = torch.zeros(B * 16, dtype=torch.int64, device="cuda")
+dbg = torch.zeros(B * 16 + 128, dtype=torch.int64, device="cuda")
 lib.mhe_diag_set_buffer(ctypes.c_void_p(dbg.data_ptr()))
 w = configs.make_c2(B=B)
 s = solver.from_workload(w)
@@ -32,10 +32,16 @@ ev0.record()
 X, c, it, st = s.solve(w.X_init, w.U, w.Y, max_iter=iters, tol=0.0)
 ev1.record()
 torch.cuda.synchronize()
-d = dbg.view(B, 16).cpu().numpy().astype(np.float64) / iters
+allv = dbg.cpu().numpy().astype(np.float64)
+d = allv[:B * 16].reshape(B, 16) / iters
+busy = allv[B * 16:].reshape(8, 16) / (iters * 3)  # block 0, summed over the launches
 names = {7: "loop head", 6: "node/meas rows", 14: "node mat-vec loop", 0: "node+meas barrier", 1: "gradient", 15: "tile build", 2: "tile barrier", 3: "chol tail", 4: "backward", 5: "exit",
-         8: "  T (trsm)", 9: "  barrier1", 12: "  U: rhs/panel", 13: "  U: slots", 10: "  U: diag", 11: "  barrier2"}
+         8: "  T (trsm) | SB: CP pre-panel", 9: "  barrier1 | SB: slowest worker busy", 12: "  U: rhs/panel", 13: "  U: slots | SB: wave 4 busy", 10: "  U: diag | SB: slowest worker over CP", 11: "  barrier2"}
 tot = d.sum(1).mean()
 print(f"B={B} iters={iters} kernel {ev0.elapsed_time(ev1):.3f} ms; cycles/iter/WG (s_memtime) total {tot:.0f}")
 for i, nm in names.items():
     print(f"  {nm:10s} {d[:, i].mean():10.0f}  ({100 * d[:, i].mean() / tot:5.1f} %)  max {d[:, i].max():.0f}")
+if busy.any():
+    print("small-batch factorization, block 0: busy cycles per interval (rows: waves 0..7, cols: k)")
+    for w in range(8):
+        print(f"  wave {w}: " + " ".join(f"{v:6.0f}" for v in busy[w][:13]) + f"   sum {busy[w].sum():7.0f}")
