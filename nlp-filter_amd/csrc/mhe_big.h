@@ -825,6 +825,18 @@ constexpr int BIG_WIDE_NT = MHE_BIG_WIDE_NT;
 #ifndef MHE_BIG_LLR8
 #define MHE_BIG_LLR8 2  // rows per wave of the left-looking update, 8-wide slab instance
 #endif
+#ifndef MHE_BIG_SPLIT
+#define MHE_BIG_SPLIT 0  // 1: the left-looking factorization as per-block-column launches (k_big_chol SPLIT, k_big_rows)
+#endif
+#ifndef MHE_BIG_ROWS_KC
+#define MHE_BIG_ROWS_KC 2  // k_big_rows: k tiles per staged slab
+#endif
+#ifndef MHE_BIG_ROWS_DB
+#define MHE_BIG_ROWS_DB 1  // k_big_rows: slabs double-buffered (the next in flight during this one's MFMAs)
+#endif
+#ifndef MHE_BIG_ROWS_XCD
+#define MHE_BIG_ROWS_XCD 1  // k_big_rows: a trajectory's row groups on one XCD (batch % 8 == 0)
+#endif
 #ifndef MHE_BIG_KO
 #define MHE_BIG_KO 0  // knock-out mask for timing probes only (tools/ko_big.sh): 1 trailing / left-looking
                       // update, 2 in-block, 4 TRSM, 8 the left-looking update's slab staging,
@@ -862,6 +874,23 @@ __device__ __forceinline__ void stage_slab(double* LJ, const double* H, int J0, 
   }
 }
 
+// stage_slab by LDS-DMA (global_load_lds_dwordx4): no VGPR holds the data, so a pass
+// with its accumulators in registers (FR) can stage without spilling them.  One wave
+// instruction moves 64 consecutive 16-B chunks (half a tile) to consecutive LDS.  The
+// caller's __syncthreads() after the vmcnt(0) makes the slab visible (wait = false: the
+// caller waits, e.g. one chunk later).
+__device__ __forceinline__ void stage_slab_lds(double* LJ, const double* H, int J0, int jb, int k0, int kb, int NT,
+                                               bool wait = true) {
+  const int nch = jb * kb * 128;  // 16-B chunks, a multiple of 64
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int c0 = wave * 64; c0 < nch; c0 += BIG_NTHREADS) {
+    const int t = c0 >> 7, jj = t / kb, kk = t - jj * kb;
+    const double* src = H + (size_t)big_tile_index(J0 + jj, k0 + kk, NT) * 256 + 2 * ((c0 & 127) + lane);
+    __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(LJ + 2 * c0), 16, 0, 0);
+  }
+  if (wait) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // LL = true: LEFT-looking updates instead of the trailing update.  Before block column
 // k0 is factored, its tiles (I, k0 .. kend-1), I >= k0, receive all their updates
 // sum_{k < k0} L_Ik L_Jk^T in one visit: a wave keeps one row's BIG_JB accumulators in
@@ -869,8 +898,14 @@ __device__ __forceinline__ void stage_slab(double* LJ, const double* H, int J0, 
 // a time.  Every tile is then read and written ONCE per factorization (the right-looking
 // update reads and writes it once per super-block above it); L_Ik is read once per block
 // column (as before) and the staged L_Jk once per group of 8 rows.
-template <int BIG_JB, bool LL = false>
-__global__ __launch_bounds__(BIG_NTHREADS, BIG_JB == 8 ? 2 : 4) void k_big_chol(BigArgs a) {
+// SPLIT (left-looking only) runs the factorization as one launch per stage instead of one
+// per trajectory: SPLIT = 1 is block column kfirst's diagonal stage (the left-looking update
+// of the block's own rows, then the diagonal block), k_big_rows the rows below it (a launch
+// of its own, one workgroup per 8 rows), SPLIT = 2 the backward solve.  SPLIT = 0: the whole
+// factorization and solve in one launch (the right-looking form, and the A/B baseline).
+template <int BIG_JB, bool LL = false, int SPLIT = 0>
+__global__ __launch_bounds__(BIG_NTHREADS, BIG_JB == 8 ? 2 : 4) void k_big_chol(BigArgs a, int kfirst) {
+  static_assert(SPLIT == 0 || LL, "the split stages are the left-looking factorization's");
   const int b = blockIdx.x;
   if (a.state[b] != BIG_RUNNING) return;
   const BigWs WL = big_ws_layout(a.P, a.M, a.n, a.NT, a.nz, a.nc);
@@ -890,7 +925,8 @@ __global__ __launch_bounds__(BIG_NTHREADS, BIG_JB == 8 ? 2 : 4) void k_big_chol(
   const int NT = a.NT;
   if (threadIdx.x == 0) *flag = 0;
   init_units(UN);
-  for (int k0 = 0; k0 < NT; k0 += BIG_KB) {
+  const int kbeg = SPLIT == 1 ? kfirst : 0, kstop = SPLIT == 1 ? min(kfirst + BIG_KB, NT) : (SPLIT == 2 ? 0 : NT);
+  for (int k0 = kbeg; k0 < kstop; k0 += BIG_KB) {
     const int kend = min(k0 + BIG_KB, NT);
     if constexpr (LL) {
       // ---- left-looking update of block column k0 by all previous columns: a wave
@@ -898,13 +934,14 @@ __global__ __launch_bounds__(BIG_NTHREADS, BIG_JB == 8 ? 2 : 4) void k_big_chol(
       constexpr int LLR = BIG_JB == 8 ? MHE_BIG_LLR8 : 2;
       for (int jh = 0; jh < kend - k0 && k0 > 0 && !(MHE_BIG_KO & 1); jh += BIG_JB) {
         const int jw = min(BIG_JB, kend - k0 - jh), Jb = k0 + jh;
-        for (int g0 = Jb; g0 < NT; g0 += BIG_NW * LLR) {
+        const int rowend = SPLIT ? kend : NT;  // SPLIT: the rows below get theirs in k_big_rows
+        for (int g0 = Jb; g0 < rowend; g0 += BIG_NW * LLR) {
           int Iq[LLR], jm[LLR];
           d4 c[LLR][BIG_JB];
 #pragma unroll
           for (int q = 0; q < LLR; ++q) {
             Iq[q] = g0 + wave + BIG_NW * q;
-            jm[q] = Iq[q] < NT ? min(jw, Iq[q] - Jb + 1) : 0;
+            jm[q] = Iq[q] < rowend ? min(jw, Iq[q] - Jb + 1) : 0;
 #pragma unroll
             for (int jj = 0; jj < BIG_JB; ++jj) {
               if (jj < jm[q]) {
@@ -1081,7 +1118,7 @@ __global__ __launch_bounds__(BIG_NTHREADS, BIG_JB == 8 ? 2 : 4) void k_big_chol(
     // next L_Ik' during in-block step kp (C4 -0.4 %); the 4-wide one loads at the point of
     // use (the prefetch registers add spills there: C3 +1.6 %, profiles/r04_ab_big_rows_prefetch.txt).
     constexpr bool RPF = BIG_JB == 8;
-    for (int I = kend + wave; I < NT && !(MHE_BIG_KO & 16); I += RPW * BIG_NW) {
+    for (int I = kend + wave; I < NT && !SPLIT && !(MHE_BIG_KO & 16); I += RPW * BIG_NW) {
       const bool two = RPW == 2 && I + BIG_NW < NT;
       const int I2 = two ? I + BIG_NW : I;
       d4 an, an2;  // A_Ik^T of the next tile, k-major (= row-major A_Ik read transposed)
@@ -1216,6 +1253,7 @@ __global__ __launch_bounds__(BIG_NTHREADS, BIG_JB == 8 ? 2 : 4) void k_big_chol(
     if (threadIdx.x == 0) a.state[b] = MHE_STATUS_NOT_SPD;
     return;
   }
+  if constexpr (SPLIT == 1) return;  // the rows below and the solve are launches of their own
   // backward: delta_k = L_kk^-T (y_k - sum_{I>k} L_Ik^T delta_I), delta in place in YV.
   // A chain of NT steps with two barriers each, so nothing on it waits for HBM: every
   // wave loads its first BWD_PF tiles of column k - 1 (and wave 0 its four L_kk^-T
@@ -1290,6 +1328,147 @@ __global__ __launch_bounds__(BIG_NTHREADS, BIG_JB == 8 ? 2 : 4) void k_big_chol(
       for (int r = 0; r < 4; ++r) cur[m][r] = nxt[m][r];
 #pragma unroll
     for (int i = 0; i < 4; ++i) lt[i] = ltn[i];
+  }
+}
+
+
+// The rows below block column k0 of the split left-looking factorization (k_big_chol
+// SPLIT = 1 has factored the block's diagonal tiles, L_kk^-T in LT, y_k in YV): one
+// workgroup per BIG_NW rows (one row per wave).  Each row's kb block-column tiles are
+// accumulated transposed in registers, c^T = A_Ik^T - sum_{k<k0} L_Jk L_Ik^T (the staged
+// L_Jk as the MFMA A operand, the row's L_Ik streamed as B), then the in-block updates and
+// the TRSM run on those registers: every L_Ik (k < k0) is read once per block column and
+// L_Ik is written once.  Same operations in the same order per element as the one-launch
+// form's left-looking pass + rows pass.
+//   staging  the kb x KC slab of L_Jk by LDS-DMA, double-buffered: chunk i + 1 is in flight
+//            while chunk i's MFMAs run (one barrier per chunk);
+//   XCD      a batch that is a multiple of 8 is remapped so all groups of a trajectory land
+//            on one XCD (dispatch is round-robin over the 8 XCDs by linear workgroup id):
+//            the slab and LB tiles every group of the trajectory stages come from that L2.
+// LDS: two slabs, then (same region) the block's in-block L tiles LB and L_kk^-T.
+__host__ __device__ constexpr int big_rows_lds() { return BIG_LB_TILES * 256 + BIG_KB * DTS; }  // doubles
+template <int KC = MHE_BIG_ROWS_KC, bool DB = MHE_BIG_ROWS_DB != 0>
+__global__ __launch_bounds__(BIG_NTHREADS, 4) void k_big_rows(BigArgs a, int k0) {
+  static_assert((DB ? 2 : 1) * BIG_KB * KC * 256 <= big_rows_lds(), "the slabs fit the LDS region");
+  const int G = gridDim.x;
+  int b = blockIdx.y, grp = blockIdx.x;
+  if (MHE_BIG_ROWS_XCD && (gridDim.y & 7) == 0) {
+    const int L = blockIdx.x + G * blockIdx.y, x = L & 7, j = L >> 3;
+    b = 8 * (j / G) + x;
+    grp = j - G * (j / G);
+  }
+  if (a.state[b] != BIG_RUNNING) return;
+  const BigWs WL = big_ws_layout(a.P, a.M, a.n, a.NT, a.nz, a.nc);
+  double* ws = a.ws + (size_t)b * a.ws_stride;
+  double* H = ws + WL.H;
+  const double* LTg = ws + WL.LT;
+  double* BV = ws + WL.BV;
+  const double* YV = ws + WL.YV;
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  double* LB = sm;
+  double* LTs = sm + BIG_LB_TILES * 256;
+  const int NT = a.NT;
+  const int kend = min(k0 + BIG_KB, NT), kb = kend - k0;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4, c = lane & 15;
+  // Branch-free over the accumulators (a conditionally updated accumulator costs phi copies
+  // of all of them): a wave without a row (I >= NT) and the columns past kb of the last
+  // block column compute on clamped, valid tiles; only stores are predicated.
+  const int I = kend + BIG_NW * grp + wave;
+  const bool act = I < NT;
+  const int Ic = act ? I : NT - 1;
+  d4 acc[BIG_KB];
+#pragma unroll
+  for (int kk = 0; kk < BIG_KB; ++kk) {
+    const double* A = H + (size_t)big_tile_index(Ic, k0 + min(kk, kb - 1), NT) * 256;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc[kk][r] = A[c * 16 + 4 * r + g];  // A_Ik^T, k-major
+  }
+  constexpr int SLAB = BIG_KB * KC * 256;
+  if (k0 > 0 && !(MHE_BIG_KO & 1)) stage_slab_lds(sm, H, k0, kb, 0, KC, NT, false);
+  for (int kc = 0; kc < k0 && !(MHE_BIG_KO & 1); kc += KC) {
+    const double* LJ = sm + (DB ? ((kc / KC) & 1) * SLAB : 0);
+    if (!DB && kc > 0) {
+      __syncthreads();  // the previous chunk's readers are done
+      stage_slab_lds(sm, H, k0, kb, kc, KC, NT, false);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this chunk's slab has landed
+    __syncthreads();  // ... for every wave, and the other buffer's last readers are done
+    if (DB && kc + KC < k0) stage_slab_lds(sm + (((kc / KC) + 1) & 1) * SLAB, H, k0, kb, kc + KC, KC, NT, false);
+    double bn[4];
+    const double* L0 = H + (size_t)big_tile_index(Ic, kc, NT) * 256;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bn[r] = L0[64 * r + lane];
+#pragma unroll
+    for (int kk = 0; kk < KC; ++kk) {
+      double bv[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bv[r] = bn[r];
+      if (kk + 1 < KC) {
+        const double* Ln = H + (size_t)big_tile_index(Ic, kc + kk + 1, NT) * 256;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bn[r] = Ln[64 * r + lane];
+      }
+      // the staged A operands one tile ahead
+      double a0[4], a1[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) a0[r] = LJ[kk * 256 + 64 * r + lane];
+#pragma unroll
+      for (int jj = 0; jj < BIG_KB; ++jj) {
+        if (jj + 1 < BIG_KB) {
+          const int jn = min(jj + 1, kb - 1);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) a1[r] = LJ[(jn * KC + kk) * 256 + 64 * r + lane];
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          acc[jj] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0[r], bv[r], acc[jj], 0, 0, MFMA_NEG_A);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) a0[r] = a1[r];
+      }
+    }
+  }
+  // the block's in-block L tiles and L_kk^-T into LDS (over the slabs)
+  __syncthreads();
+  for (int e = threadIdx.x; e < (kb * (kb - 1) / 2) * 128; e += BIG_NTHREADS) {
+    const int slot = e >> 7;
+    int ii = 1;  // slot = ii (ii - 1) / 2 + kp, kp < ii
+    while (ii * (ii + 1) / 2 <= slot) ++ii;
+    const int kp = slot - ii * (ii - 1) / 2;
+    const double2 w = *(const double2*)(H + (size_t)big_tile_index(k0 + ii, k0 + kp, NT) * 256 + 2 * (e & 127));
+    *(double2*)(LB + 256 * slot + 2 * (e & 127)) = w;
+  }
+  for (int e = threadIdx.x; e < kb * DTS; e += BIG_NTHREADS) LTs[e] = LTg[(size_t)k0 * DTS + e];
+  __syncthreads();
+#pragma unroll
+  for (int kk = 0; kk < BIG_KB; ++kk) {
+    d4 cc = acc[kk];
+#pragma unroll
+    for (int kp = 0; kp < kk; ++kp) {
+      const double* Lk = LB + (kk * (kk - 1) / 2 + kp) * 256;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        cc = __builtin_amdgcn_mfma_f64_16x16x4f64(Lk[64 * r + lane], acc[kp][r], cc, 0, 0, MFMA_NEG_A);
+    }
+    const double* LT = LTs + kk * DTS;
+    d4 t = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) t = __builtin_amdgcn_mfma_f64_16x16x4f64(LT[(4 * r + g) * LIS + c], cc[r], t, 0, 0, 0);
+    acc[kk] = t;
+    const int k = k0 + min(kk, kb - 1);
+    int go = g;  // opaque per step: the y addresses are not hoisted (8 x 4 of them)
+    asm volatile("" : "+v"(go));
+    const double* yk = YV + 16 * k;
+    const double y0 = yk[go], y1 = yk[go + 4], y2 = yk[go + 8], y3 = yk[go + 12];
+    double s = t[0] * y0 + t[1] * y1 + t[2] * y2 + t[3] * y3;
+    s += __shfl_xor(s, 16);
+    s += __shfl_xor(s, 32);
+    if (act && kk < kb) {
+      double* Ak = H + (size_t)big_tile_index(I, k0 + kk, NT) * 256;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Ak[64 * r + lane] = t[r];
+      if (lane < 16) BV[16 * I + lane] -= s;
+    }
   }
 }
 

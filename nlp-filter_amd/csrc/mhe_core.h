@@ -2495,19 +2495,49 @@ int launch_build_cc(const mhe_dims* dm, int NT, const double* D, const double* c
   }
 }
 
-// The factorization instance of the large-system path and its LDS bytes: left-looking
-// block-column updates (default; 38 % less HBM traffic than the right-looking trailing
-// update, C3 +5 %, C4 +7.5 %, C5 +8 %); the right-looking form (bitwise-identical
-// iterates, tests/test_gpu_big.py) only when a caller selected it explicitly with
-// mhe_set_option(MHE_OPT_BIG_RIGHT_LOOKING, 1)
-inline int big_chol_kernel(const BigArgs& A, void (**chol)(BigArgs)) {
+// The factorization of the large-system path: left-looking block-column updates (default;
+// 38 % less HBM traffic than the right-looking trailing update, C3 +5 %, C4 +7.5 %, C5 +8 %);
+// the right-looking form (bitwise-identical iterates, tests/test_gpu_big.py) only when a
+// caller selected it with mhe_set_option(MHE_OPT_BIG_RIGHT_LOOKING, 1).  MHE_BIG_SPLIT: the
+// left-looking form as launches per block column (k_big_chol SPLIT = 1, then k_big_rows over
+// the rows below, one workgroup per 8 rows) and one for the solve (SPLIT = 2).
+struct BigCholPlan {
+  void (*mono)(BigArgs, int);
+  void (*diag)(BigArgs, int);
+  void (*bwd)(BigArgs, int);
+  int smem, smem_rows;
+  bool split;
+};
+inline int big_chol_plan(const BigArgs& A, BigCholPlan& p) {
   const bool wide = A.NT >= BIG_WIDE_NT;
-  const int smem = big_chol_lds(wide ? 8 : 4) * (int)sizeof(double);
+  p.smem = big_chol_lds(wide ? 8 : 4) * (int)sizeof(double);
+  p.smem_rows = big_rows_lds() * (int)sizeof(double);
   const bool ll = g_opt_big_right_looking == 0;
-  *chol = wide ? (ll ? k_big_chol<8, true> : k_big_chol<8>) : (ll ? k_big_chol<4, true> : k_big_chol<4>);
-  if (hipFuncSetAttribute((const void*)*chol, hipFuncAttributeMaxDynamicSharedMemorySize, smem) != hipSuccess)
+  p.split = ll && MHE_BIG_SPLIT != 0;
+  p.mono = wide ? (ll ? k_big_chol<8, true> : k_big_chol<8>) : (ll ? k_big_chol<4, true> : k_big_chol<4>);
+  p.diag = wide ? k_big_chol<8, true, 1> : k_big_chol<4, true, 1>;
+  p.bwd = wide ? k_big_chol<8, true, 2> : k_big_chol<4, true, 2>;
+  for (auto f : {p.mono, p.diag, p.bwd})
+    if (hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, p.smem) != hipSuccess)
+      return -1;
+  if (hipFuncSetAttribute((const void*)k_big_rows<>, hipFuncAttributeMaxDynamicSharedMemorySize, p.smem_rows) !=
+      hipSuccess)
     return -1;
-  return smem;
+  return 0;
+}
+inline void launch_big_factor(const BigCholPlan& p, const BigArgs& A, int batch, hipStream_t st) {
+  if (!p.split) {
+    hipLaunchKernelGGL(p.mono, dim3(batch), dim3(BIG_NTHREADS), p.smem, st, A, 0);
+    return;
+  }
+  for (int k0 = 0; k0 < A.NT; k0 += BIG_KB) {
+    hipLaunchKernelGGL(p.diag, dim3(batch), dim3(BIG_NTHREADS), p.smem, st, A, k0);
+    const int kend = k0 + BIG_KB < A.NT ? k0 + BIG_KB : A.NT;
+    if (kend < A.NT)
+      hipLaunchKernelGGL(k_big_rows<>, dim3((A.NT - kend + BIG_NW - 1) / BIG_NW, batch), dim3(BIG_NTHREADS),
+                         p.smem_rows, st, A, k0);
+  }
+  hipLaunchKernelGGL(p.bwd, dim3(batch), dim3(BIG_NTHREADS), p.smem, st, A, 0);
 }
 
 // k_big_assemble's launch shape: per tile position ceil(nchl / WPB) workgroups of WPB
@@ -2539,10 +2569,9 @@ int launch_big_stage(const mhe_dims* dm, BigArgs& A, int batch, int stage, hipSt
     hipLaunchKernelGGL((k_big_resid<DYN, MEAS>), dim3(batch), dim3(BIG_NTHREADS), 0, st, A, 0);
     hipLaunchKernelGGL((k_big_assemble<DYN, MEAS>), dim3(sh.blocks, batch), dim3(64 * sh.wpb), sh.lds, st, A);
   } else {
-    void (*chol)(BigArgs) = nullptr;
-    const int smem = big_chol_kernel(A, &chol);
-    if (smem < 0) return MHE_ERR_HIP;
-    hipLaunchKernelGGL(chol, dim3(batch), dim3(BIG_NTHREADS), smem, st, A);
+    BigCholPlan cp;
+    if (big_chol_plan(A, cp) < 0) return MHE_ERR_HIP;
+    launch_big_factor(cp, A, batch, st);
   }
   return hipGetLastError() == hipSuccess ? MHE_OK : MHE_ERR_HIP;
 }
@@ -2550,9 +2579,8 @@ int launch_big_stage(const mhe_dims* dm, BigArgs& A, int batch, int stage, hipSt
 template <class DYN, class MEAS>
 int launch_big(const mhe_dims* dm, BigArgs& A, int batch, int max_iter, hipStream_t st) {
   big_pair_plan(A, BigGSupport<MEAS>::get(A.idx, A.n));
-  void (*chol)(BigArgs) = nullptr;
-  const int smem = big_chol_kernel(A, &chol);
-  if (smem < 0) return MHE_ERR_HIP;
+  BigCholPlan cp;
+  if (big_chol_plan(A, cp) < 0) return MHE_ERR_HIP;
   const int K = A.nz + A.nc;
   const int smem_b = (K * K + 2 * K) * (int)sizeof(double);
   if (K > 0 && hipFuncSetAttribute((const void*)k_big_border<DYN::n, MEAS::p>,
@@ -2572,7 +2600,7 @@ int launch_big(const mhe_dims* dm, BigArgs& A, int batch, int max_iter, hipStrea
   for (int it = 0; it < max_iter; ++it) {
     hipLaunchKernelGGL((k_big_resid<DYN, MEAS>), dim3(batch), dim3(BIG_NTHREADS), 0, st, A, 0);
     hipLaunchKernelGGL((k_big_assemble<DYN, MEAS>), dim3(sh.blocks, batch), dim3(64 * sh.wpb), sh.lds, st, A);
-    hipLaunchKernelGGL(chol, dim3(batch), dim3(BIG_NTHREADS), smem, st, A);
+    launch_big_factor(cp, A, batch, st);
     if (K > 0) hipLaunchKernelGGL((k_big_border<DYN::n, MEAS::p>), dim3(batch), dim3(BIG_NTHREADS), smem_b, st, A);
     if (bounded)
       hipLaunchKernelGGL((k_big_linesearch<DYN, MEAS>), dim3(batch), dim3(BIG_NTHREADS), smem_ls, st, A);
