@@ -826,13 +826,14 @@ constexpr int BIG_WIDE_NT = MHE_BIG_WIDE_NT;
 #define MHE_BIG_LLR8 2  // rows per wave of the left-looking update, 8-wide slab instance
 #endif
 #ifndef MHE_BIG_SPLIT
-#define MHE_BIG_SPLIT 0  // 1: the left-looking factorization as per-block-column launches (k_big_chol SPLIT, k_big_rows)
+#define MHE_BIG_SPLIT 2  // the left-looking factorization as per-block-column launches (k_big_chol SPLIT,
+                         // k_big_rows): 2 = for wide systems (NT >= BIG_WIDE_NT: C4, C5), 1 = always, 0 = never
 #endif
 #ifndef MHE_BIG_ROWS_KC
-#define MHE_BIG_ROWS_KC 2  // k_big_rows: k tiles per staged slab
+#define MHE_BIG_ROWS_KC 4  // k_big_rows: k tiles per staged slab
 #endif
 #ifndef MHE_BIG_ROWS_DB
-#define MHE_BIG_ROWS_DB 1  // k_big_rows: slabs double-buffered (the next in flight during this one's MFMAs)
+#define MHE_BIG_ROWS_DB 0  // k_big_rows: slabs double-buffered (the next in flight during this one's MFMAs)
 #endif
 #ifndef MHE_BIG_ROWS_XCD
 #define MHE_BIG_ROWS_XCD 1  // k_big_rows: a trajectory's row groups on one XCD (batch % 8 == 0)
@@ -891,6 +892,196 @@ __device__ __forceinline__ void stage_slab_lds(double* LJ, const double* H, int 
   if (wait) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// Block column k0 of the left-looking factorization up to its diagonal block: the
+// left-looking update of the column's tiles (rows < rowend: all rows in the one-launch
+// form, the block's own rows in the split one), then the diagonal block (panels on wave 0,
+// in-block updates and TRSM on the others; L_Ik to H and LB, L_kk^-T to LT and LTs, y_k to
+// YV, b_I updated).  LDS as k_big_chol's (DT, flag, UN, LJ); a non-SPD pivot sets *flag.
+template <int BIG_JB, bool LL, bool SPLITROWS>
+__device__ __forceinline__ void big_diag_block(const BigArgs& a, int k0, int kend, double* H, double* LTg, double* BV,
+                                               double* YV, double* sm, int lane, int wave) {
+  double* DT = sm;
+  int* flag = (int*)(sm + DTS + BIG_NW * 16 + 16);
+  double* UN = sm + DTS + BIG_NW * 16 + 16 + 2;
+  double* LJ = UN + UNITS;
+  const int NT = a.NT;
+  if constexpr (LL) {
+    // ---- left-looking update of block column k0 by all previous columns: a wave
+    // takes LLR rows (g0 + wave + 8 q), so one staged slab serves 8 LLR rows
+    constexpr int LLR = BIG_JB == 8 ? MHE_BIG_LLR8 : 2;
+    for (int jh = 0; jh < kend - k0 && k0 > 0 && !(MHE_BIG_KO & 1); jh += BIG_JB) {
+      const int jw = min(BIG_JB, kend - k0 - jh), Jb = k0 + jh;
+      const int rowend = SPLITROWS ? kend : NT;  // split: the rows below get theirs in k_big_rows
+      for (int g0 = Jb; g0 < rowend; g0 += BIG_NW * LLR) {
+        int Iq[LLR], jm[LLR];
+        d4 c[LLR][BIG_JB];
+#pragma unroll
+        for (int q = 0; q < LLR; ++q) {
+          Iq[q] = g0 + wave + BIG_NW * q;
+          jm[q] = Iq[q] < rowend ? min(jw, Iq[q] - Jb + 1) : 0;
+#pragma unroll
+          for (int jj = 0; jj < BIG_JB; ++jj) {
+            if (jj < jm[q]) {
+              const double* C = H + (size_t)big_tile_index(Iq[q], Jb + jj, NT) * 256;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) c[q][jj][r] = C[64 * r + lane];
+            }
+          }
+        }
+        for (int kc = 0; kc < k0; kc += BIG_KB) {
+          __syncthreads();  // the previous chunk's slab is consumed
+          if (!(MHE_BIG_KO & 8)) stage_slab(LJ, H, Jb, jw, kc, BIG_KB, NT);  // L_Jk, jj < jw, kk < BIG_KB
+          __syncthreads();
+          // both rows share each staged B operand (one LDS read per 2 x 4 MFMAs); the
+          // rows' next L_Ik tiles are loaded one k step ahead
+          double av[LLR][4];
+#pragma unroll
+          for (int q = 0; q < LLR; ++q) {
+            const double* LI0 = H + (size_t)big_tile_index(jm[q] > 0 ? Iq[q] : Jb, kc, NT) * 256;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) av[q][r] = LI0[64 * r + lane];  // negated by the MFMA
+          }
+#pragma unroll 1
+          for (int kk = 0; kk < BIG_KB; ++kk) {
+            double an[LLR][4];
+#pragma unroll
+            for (int q = 0; q < LLR; ++q) {
+              const double* LIn =
+                  H + (size_t)big_tile_index(jm[q] > 0 ? Iq[q] : Jb, kc + min(kk + 1, BIG_KB - 1), NT) * 256;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) an[q][r] = LIn[64 * r + lane];
+            }
+#pragma unroll
+            for (int jj = 0; jj < BIG_JB; ++jj) {
+              if (jj < jm[0]) {  // rows ascend with q: jm[0] <= jm[1]
+                const double* Bt = LJ + (jj * BIG_KB + kk) * 256;
+                double bv[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) bv[r] = Bt[64 * r + lane];
+#pragma unroll
+                for (int q = 0; q < LLR; ++q) {
+                  if (jj < jm[q]) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                      c[q][jj] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[q][r], bv[r], c[q][jj], 0, 0, MFMA_NEG_A);
+                  }
+                }
+              } else if (jj < jm[LLR - 1]) {
+                const double* Bt = LJ + (jj * BIG_KB + kk) * 256;
+                double bv[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) bv[r] = Bt[64 * r + lane];
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                  c[LLR - 1][jj] =
+                      __builtin_amdgcn_mfma_f64_16x16x4f64(av[LLR - 1][r], bv[r], c[LLR - 1][jj], 0, 0, MFMA_NEG_A);
+              }
+            }
+#pragma unroll
+            for (int q = 0; q < LLR; ++q)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) av[q][r] = an[q][r];
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < LLR; ++q) {
+#pragma unroll
+          for (int jj = 0; jj < BIG_JB; ++jj) {
+            if (jj < jm[q]) {
+              double* C = H + (size_t)big_tile_index(Iq[q], Jb + jj, NT) * 256;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) C[64 * r + lane] = c[q][jj][r];
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();  // the block column is up to date; LJ is free for LB / LTs
+  }
+  // ---- diagonal block, left-looking inside the block column: at step k every tile
+  // (I, k), k <= I < kend, gets all of its in-block updates in ONE pass (K = 16 (k - k0),
+  // L_kk' operands from LDS), then the TRSM.  Two workgroup barriers per k.
+  // LB (= the LJ region, free until the trailing phase): L_Ik' for k0 <= k' < I < kend, packed
+  // strictly-lower: slot (I - k0)(I - k0 - 1)/2 + (k' - k0); LTs: L_kk^-T of the block's k.
+  double* LB = LJ;
+  double* LTs = LJ + BIG_LB_TILES * 256;
+  for (int k = k0; k < kend; ++k) {
+    const int nk = k - k0;
+    if (wave == 0) {
+      // diagonal tile: A_kk - sum L_kk' L_kk'^T -> DT, panel, y_k
+      const double* Akk = H + (size_t)big_tile_index(k, k, NT) * 256;
+      d4 c;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) c[r] = Akk[64 * r + lane];
+      for (int kk = 0; kk < nk && !(MHE_BIG_KO & 2); ++kk) {
+        const double* Lt = LB + (nk * (nk - 1) / 2 + kk) * 256;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const double v = Lt[64 * r + lane];
+          c = __builtin_amdgcn_mfma_f64_16x16x4f64(v, v, c, 0, 0, MFMA_NEG_A);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) DT[64 * r + lane] = c[r];
+      wave_lds_sync();
+      const bool bad = panel(DT, UN, lane);
+      if (bad && lane == 0 && !MHE_BIG_KO) *flag = 1;  // probes keep every trajectory running
+      wave_lds_sync();
+      block_fwd(DT, BV + 16 * k, YV + 16 * k, lane);  // y_k = L_kk^-1 b_k
+      for (int e = lane; e < DTS; e += 64) {
+        LTg[(size_t)k * DTS + e] = DT[e];
+        LTs[nk * DTS + e] = DT[e];
+      }
+    } else {
+      // block rows k < I < kend: c' = A_Ik^T - sum_k' L_kk' L_Ik'^T, stored k-major in place (= A_Ik^T row-major)
+      for (int I = k + wave; I < kend; I += BIG_NW - 1) {
+        double* Ak = H + (size_t)big_tile_index(I, k, NT) * 256;
+        d4 c;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) c[r] = Ak[(lane & 15) * 16 + 4 * r + (lane >> 4)];
+        for (int kk = 0; kk < nk && !(MHE_BIG_KO & 2); ++kk) {
+          const double* Lk = LB + (nk * (nk - 1) / 2 + kk) * 256;
+          const double* LI = LB + ((I - k0) * (I - k0 - 1) / 2 + kk) * 256;
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            c = __builtin_amdgcn_mfma_f64_16x16x4f64(Lk[64 * r + lane], LI[64 * r + lane], c, 0, 0, MFMA_NEG_A);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Ak[64 * r + lane] = c[r];
+      }
+    }
+    __syncthreads();
+    if (*flag) break;
+    // TRSM: L_Ik^T = L_kk^-1 A_Ik^T (k-major result) for the block rows, b_I -= L_Ik y_k; L_Ik also to LB
+    const double yk = YV[16 * k + (lane >> 4)], yk1 = YV[16 * k + 4 + (lane >> 4)],
+                 yk2 = YV[16 * k + 8 + (lane >> 4)], yk3 = YV[16 * k + 12 + (lane >> 4)];
+    for (int I = k + 1 + wave; I < kend && !(MHE_BIG_KO & 4); I += BIG_NW) {
+      double* Ak = H + (size_t)big_tile_index(I, k, NT) * 256;
+      double av[4], bv[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        av[r] = DT[(4 * r + (lane >> 4)) * LIS + (lane & 15)];  // L_kk^-1 [lane & 15][4r + (lane >> 4)]
+        bv[r] = Ak[64 * r + lane];
+      }
+      d4 u = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) u = __builtin_amdgcn_mfma_f64_16x16x4f64(av[r], bv[r], u, 0, 0, 0);
+      // u[r] = L_Ik[lane & 15][(lane >> 4) + 4 r]
+      double* LBs = LB + ((I - k0) * (I - k0 - 1) / 2 + nk) * 256;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        Ak[64 * r + lane] = u[r];
+        LBs[64 * r + lane] = u[r];
+      }
+      double s = u[0] * yk + u[1] * yk1 + u[2] * yk2 + u[3] * yk3;
+      s += __shfl_xor(s, 16);
+      s += __shfl_xor(s, 32);
+      if (lane < 16) BV[16 * I + lane] -= s;
+    }
+    __syncthreads();
+  }
+}
+
 // LL = true: LEFT-looking updates instead of the trailing update.  Before block column
 // k0 is factored, its tiles (I, k0 .. kend-1), I >= k0, receive all their updates
 // sum_{k < k0} L_Ik L_Jk^T in one visit: a wave keeps one row's BIG_JB accumulators in
@@ -928,181 +1119,9 @@ __global__ __launch_bounds__(BIG_NTHREADS, BIG_JB == 8 ? 2 : 4) void k_big_chol(
   const int kbeg = SPLIT == 1 ? kfirst : 0, kstop = SPLIT == 1 ? min(kfirst + BIG_KB, NT) : (SPLIT == 2 ? 0 : NT);
   for (int k0 = kbeg; k0 < kstop; k0 += BIG_KB) {
     const int kend = min(k0 + BIG_KB, NT);
-    if constexpr (LL) {
-      // ---- left-looking update of block column k0 by all previous columns: a wave
-      // takes LLR rows (g0 + wave + 8 q), so one staged slab serves 8 LLR rows
-      constexpr int LLR = BIG_JB == 8 ? MHE_BIG_LLR8 : 2;
-      for (int jh = 0; jh < kend - k0 && k0 > 0 && !(MHE_BIG_KO & 1); jh += BIG_JB) {
-        const int jw = min(BIG_JB, kend - k0 - jh), Jb = k0 + jh;
-        const int rowend = SPLIT ? kend : NT;  // SPLIT: the rows below get theirs in k_big_rows
-        for (int g0 = Jb; g0 < rowend; g0 += BIG_NW * LLR) {
-          int Iq[LLR], jm[LLR];
-          d4 c[LLR][BIG_JB];
-#pragma unroll
-          for (int q = 0; q < LLR; ++q) {
-            Iq[q] = g0 + wave + BIG_NW * q;
-            jm[q] = Iq[q] < rowend ? min(jw, Iq[q] - Jb + 1) : 0;
-#pragma unroll
-            for (int jj = 0; jj < BIG_JB; ++jj) {
-              if (jj < jm[q]) {
-                const double* C = H + (size_t)big_tile_index(Iq[q], Jb + jj, NT) * 256;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) c[q][jj][r] = C[64 * r + lane];
-              }
-            }
-          }
-          for (int kc = 0; kc < k0; kc += BIG_KB) {
-            __syncthreads();  // the previous chunk's slab is consumed
-            if (!(MHE_BIG_KO & 8)) stage_slab(LJ, H, Jb, jw, kc, BIG_KB, NT);  // L_Jk, jj < jw, kk < BIG_KB
-            __syncthreads();
-            // both rows share each staged B operand (one LDS read per 2 x 4 MFMAs); the
-            // rows' next L_Ik tiles are loaded one k step ahead
-            double av[LLR][4];
-#pragma unroll
-            for (int q = 0; q < LLR; ++q) {
-              const double* LI0 = H + (size_t)big_tile_index(jm[q] > 0 ? Iq[q] : Jb, kc, NT) * 256;
-#pragma unroll
-              for (int r = 0; r < 4; ++r) av[q][r] = LI0[64 * r + lane];  // negated by the MFMA
-            }
-#pragma unroll 1
-            for (int kk = 0; kk < BIG_KB; ++kk) {
-              double an[LLR][4];
-#pragma unroll
-              for (int q = 0; q < LLR; ++q) {
-                const double* LIn =
-                    H + (size_t)big_tile_index(jm[q] > 0 ? Iq[q] : Jb, kc + min(kk + 1, BIG_KB - 1), NT) * 256;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) an[q][r] = LIn[64 * r + lane];
-              }
-#pragma unroll
-              for (int jj = 0; jj < BIG_JB; ++jj) {
-                if (jj < jm[0]) {  // rows ascend with q: jm[0] <= jm[1]
-                  const double* Bt = LJ + (jj * BIG_KB + kk) * 256;
-                  double bv[4];
-#pragma unroll
-                  for (int r = 0; r < 4; ++r) bv[r] = Bt[64 * r + lane];
-#pragma unroll
-                  for (int q = 0; q < LLR; ++q) {
-                    if (jj < jm[q]) {
-#pragma unroll
-                      for (int r = 0; r < 4; ++r)
-                        c[q][jj] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[q][r], bv[r], c[q][jj], 0, 0, MFMA_NEG_A);
-                    }
-                  }
-                } else if (jj < jm[LLR - 1]) {
-                  const double* Bt = LJ + (jj * BIG_KB + kk) * 256;
-                  double bv[4];
-#pragma unroll
-                  for (int r = 0; r < 4; ++r) bv[r] = Bt[64 * r + lane];
-#pragma unroll
-                  for (int r = 0; r < 4; ++r)
-                    c[LLR - 1][jj] =
-                        __builtin_amdgcn_mfma_f64_16x16x4f64(av[LLR - 1][r], bv[r], c[LLR - 1][jj], 0, 0, MFMA_NEG_A);
-                }
-              }
-#pragma unroll
-              for (int q = 0; q < LLR; ++q)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) av[q][r] = an[q][r];
-            }
-          }
-#pragma unroll
-          for (int q = 0; q < LLR; ++q) {
-#pragma unroll
-            for (int jj = 0; jj < BIG_JB; ++jj) {
-              if (jj < jm[q]) {
-                double* C = H + (size_t)big_tile_index(Iq[q], Jb + jj, NT) * 256;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) C[64 * r + lane] = c[q][jj][r];
-              }
-            }
-          }
-        }
-      }
-      __syncthreads();  // the block column is up to date; LJ is free for LB / LTs
-    }
-    // ---- diagonal block, left-looking inside the block column: at step k every tile
-    // (I, k), k <= I < kend, gets all of its in-block updates in ONE pass (K = 16 (k - k0),
-    // L_kk' operands from LDS), then the TRSM.  Two workgroup barriers per k.
-    // LB (= the LJ region, free until the trailing phase): L_Ik' for k0 <= k' < I < kend, packed
-    // strictly-lower: slot (I - k0)(I - k0 - 1)/2 + (k' - k0); LTs: L_kk^-T of the block's k.
-    double* LB = LJ;
+    big_diag_block<BIG_JB, LL, SPLIT != 0>(a, k0, kend, H, LTg, BV, YV, sm, lane, wave);
+    double* LB = LJ;  // the diagonal block's L_Ik' and L_kk^-T (big_diag_block)
     double* LTs = LJ + BIG_LB_TILES * 256;
-    for (int k = k0; k < kend; ++k) {
-      const int nk = k - k0;
-      if (wave == 0) {
-        // diagonal tile: A_kk - sum L_kk' L_kk'^T -> DT, panel, y_k
-        const double* Akk = H + (size_t)big_tile_index(k, k, NT) * 256;
-        d4 c;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) c[r] = Akk[64 * r + lane];
-        for (int kk = 0; kk < nk && !(MHE_BIG_KO & 2); ++kk) {
-          const double* Lt = LB + (nk * (nk - 1) / 2 + kk) * 256;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const double v = Lt[64 * r + lane];
-            c = __builtin_amdgcn_mfma_f64_16x16x4f64(v, v, c, 0, 0, MFMA_NEG_A);
-          }
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) DT[64 * r + lane] = c[r];
-        wave_lds_sync();
-        const bool bad = panel(DT, UN, lane);
-        if (bad && lane == 0 && !MHE_BIG_KO) *flag = 1;  // probes keep every trajectory running
-        wave_lds_sync();
-        block_fwd(DT, BV + 16 * k, YV + 16 * k, lane);  // y_k = L_kk^-1 b_k
-        for (int e = lane; e < DTS; e += 64) {
-          LTg[(size_t)k * DTS + e] = DT[e];
-          LTs[nk * DTS + e] = DT[e];
-        }
-      } else {
-        // block rows k < I < kend: c' = A_Ik^T - sum_k' L_kk' L_Ik'^T, stored k-major in place (= A_Ik^T row-major)
-        for (int I = k + wave; I < kend; I += BIG_NW - 1) {
-          double* Ak = H + (size_t)big_tile_index(I, k, NT) * 256;
-          d4 c;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) c[r] = Ak[(lane & 15) * 16 + 4 * r + (lane >> 4)];
-          for (int kk = 0; kk < nk && !(MHE_BIG_KO & 2); ++kk) {
-            const double* Lk = LB + (nk * (nk - 1) / 2 + kk) * 256;
-            const double* LI = LB + ((I - k0) * (I - k0 - 1) / 2 + kk) * 256;
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-              c = __builtin_amdgcn_mfma_f64_16x16x4f64(Lk[64 * r + lane], LI[64 * r + lane], c, 0, 0, MFMA_NEG_A);
-          }
-#pragma unroll
-          for (int r = 0; r < 4; ++r) Ak[64 * r + lane] = c[r];
-        }
-      }
-      __syncthreads();
-      if (*flag) break;
-      // TRSM: L_Ik^T = L_kk^-1 A_Ik^T (k-major result) for the block rows, b_I -= L_Ik y_k; L_Ik also to LB
-      const double yk = YV[16 * k + (lane >> 4)], yk1 = YV[16 * k + 4 + (lane >> 4)],
-                   yk2 = YV[16 * k + 8 + (lane >> 4)], yk3 = YV[16 * k + 12 + (lane >> 4)];
-      for (int I = k + 1 + wave; I < kend && !(MHE_BIG_KO & 4); I += BIG_NW) {
-        double* Ak = H + (size_t)big_tile_index(I, k, NT) * 256;
-        double av[4], bv[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          av[r] = DT[(4 * r + (lane >> 4)) * LIS + (lane & 15)];  // L_kk^-1 [lane & 15][4r + (lane >> 4)]
-          bv[r] = Ak[64 * r + lane];
-        }
-        d4 u = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int r = 0; r < 4; ++r) u = __builtin_amdgcn_mfma_f64_16x16x4f64(av[r], bv[r], u, 0, 0, 0);
-        // u[r] = L_Ik[lane & 15][(lane >> 4) + 4 r]
-        double* LBs = LB + ((I - k0) * (I - k0 - 1) / 2 + nk) * 256;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          Ak[64 * r + lane] = u[r];
-          LBs[64 * r + lane] = u[r];
-        }
-        double s = u[0] * yk + u[1] * yk1 + u[2] * yk2 + u[3] * yk3;
-        s += __shfl_xor(s, 16);
-        s += __shfl_xor(s, 32);
-        if (lane < 16) BV[16 * I + lane] -= s;
-      }
-      __syncthreads();
-    }
     if (*flag) break;
     // ---- rows below the block, one wave per row: the same operations per element as
     // the diagonal block's (in-block updates in k' order, TRSM, b_I update in k order),

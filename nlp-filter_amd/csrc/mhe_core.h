@@ -2500,7 +2500,8 @@ int launch_build_cc(const mhe_dims* dm, int NT, const double* D, const double* c
 // the right-looking form (bitwise-identical iterates, tests/test_gpu_big.py) only when a
 // caller selected it with mhe_set_option(MHE_OPT_BIG_RIGHT_LOOKING, 1).  MHE_BIG_SPLIT: the
 // left-looking form as launches per block column (k_big_chol SPLIT = 1, then k_big_rows over
-// the rows below, one workgroup per 8 rows) and one for the solve (SPLIT = 2).
+// the rows below, one workgroup per 8 rows) and one for the solve (SPLIT = 2) -- for wide
+// systems by default: C4 +8.9 %, C5 +8.2 %, but C3 -5 % (profiles/r05_ab_big_split.txt).
 struct BigCholPlan {
   void (*mono)(BigArgs, int);
   void (*diag)(BigArgs, int);
@@ -2513,7 +2514,7 @@ inline int big_chol_plan(const BigArgs& A, BigCholPlan& p) {
   p.smem = big_chol_lds(wide ? 8 : 4) * (int)sizeof(double);
   p.smem_rows = big_rows_lds() * (int)sizeof(double);
   const bool ll = g_opt_big_right_looking == 0;
-  p.split = ll && MHE_BIG_SPLIT != 0;
+  p.split = ll && (MHE_BIG_SPLIT == 1 || (MHE_BIG_SPLIT == 2 && wide));
   p.mono = wide ? (ll ? k_big_chol<8, true> : k_big_chol<8>) : (ll ? k_big_chol<4, true> : k_big_chol<4>);
   p.diag = wide ? k_big_chol<8, true, 1> : k_big_chol<4, true, 1>;
   p.bwd = wide ? k_big_chol<8, true, 2> : k_big_chol<4, true, 2>;
