@@ -829,6 +829,9 @@ constexpr int BIG_WIDE_NT = MHE_BIG_WIDE_NT;
 #define MHE_BIG_SPLIT 2  // the left-looking factorization as per-block-column launches (k_big_chol SPLIT,
                          // k_big_rows): 2 = for wide systems (NT >= BIG_WIDE_NT: C4, C5), 1 = always, 0 = never
 #endif
+#ifndef MHE_BIG_TWO_STREAMS
+#define MHE_BIG_TWO_STREAMS 0  // split factorization: the batch's two halves on two streams (C3 +1.4 %, C4 +0.8 %, C5 0 vs one stream)
+#endif
 #ifndef MHE_BIG_ROWS_KC
 #define MHE_BIG_ROWS_KC 4  // k_big_rows: k tiles per staged slab
 #endif

@@ -2526,19 +2526,64 @@ inline int big_chol_plan(const BigArgs& A, BigCholPlan& p) {
     return -1;
   return 0;
 }
+// One half of the batch through the split stages (trajectories boff .. boff + nb - 1).
+inline void launch_big_split(const BigCholPlan& p, BigArgs A, int boff, int nb, hipStream_t st) {
+  A.ws += (size_t)boff * A.ws_stride;  // the stages index trajectories by workgroup only
+  A.state += boff;
+  for (int k0 = 0; k0 < A.NT; k0 += BIG_KB) {
+    hipLaunchKernelGGL(p.diag, dim3(nb), dim3(BIG_NTHREADS), p.smem, st, A, k0);
+    const int kend = k0 + BIG_KB < A.NT ? k0 + BIG_KB : A.NT;
+    if (kend < A.NT)
+      hipLaunchKernelGGL(k_big_rows<>, dim3((A.NT - kend + BIG_NW - 1) / BIG_NW, nb), dim3(BIG_NTHREADS),
+                         p.smem_rows, st, A, k0);
+  }
+  hipLaunchKernelGGL(p.bwd, dim3(nb), dim3(BIG_NTHREADS), p.smem, st, A, 0);
+}
+
+// The second stream and fork / join events of the two-stream split factorization, one set
+// per device, created on first use (nullptr: run on one stream).
+struct BigAux {
+  hipStream_t s2;
+  hipEvent_t fork, join;
+};
+inline BigAux* big_aux() {
+  static BigAux aux[16];
+  static int made[16] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return nullptr;
+  if (!made[dev]) {
+    if (hipStreamCreateWithFlags(&aux[dev].s2, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&aux[dev].fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&aux[dev].join, hipEventDisableTiming) != hipSuccess)
+      return nullptr;
+    made[dev] = 1;
+  }
+  return &aux[dev];
+}
+
+// The factorization + solve.  Split: the two halves of the batch go through the stages on
+// two streams, so one half's latency-bound diagonal stages and solve overlap the other
+// half's row launches (what the one-launch kernel gets from trajectories at different
+// phases) -- MHE_BIG_TWO_STREAMS.
 inline void launch_big_factor(const BigCholPlan& p, const BigArgs& A, int batch, hipStream_t st) {
   if (!p.split) {
     hipLaunchKernelGGL(p.mono, dim3(batch), dim3(BIG_NTHREADS), p.smem, st, A, 0);
     return;
   }
-  for (int k0 = 0; k0 < A.NT; k0 += BIG_KB) {
-    hipLaunchKernelGGL(p.diag, dim3(batch), dim3(BIG_NTHREADS), p.smem, st, A, k0);
-    const int kend = k0 + BIG_KB < A.NT ? k0 + BIG_KB : A.NT;
-    if (kend < A.NT)
-      hipLaunchKernelGGL(k_big_rows<>, dim3((A.NT - kend + BIG_NW - 1) / BIG_NW, batch), dim3(BIG_NTHREADS),
-                         p.smem_rows, st, A, k0);
+  BigAux* aux = MHE_BIG_TWO_STREAMS && batch >= 16 ? big_aux() : nullptr;
+  if (!aux) {
+    launch_big_split(p, A, 0, batch, st);
+    return;
   }
-  hipLaunchKernelGGL(p.bwd, dim3(batch), dim3(BIG_NTHREADS), p.smem, st, A, 0);
+  const int h = ((batch / 2) + 7) & ~7;  // a multiple of 8 (k_big_rows' XCD grouping)
+  if (hipEventRecord(aux->fork, st) != hipSuccess || hipStreamWaitEvent(aux->s2, aux->fork, 0) != hipSuccess) {
+    launch_big_split(p, A, 0, batch, st);
+    return;
+  }
+  launch_big_split(p, A, 0, h, st);
+  launch_big_split(p, A, h, batch - h, aux->s2);
+  if (hipEventRecord(aux->join, aux->s2) != hipSuccess || hipStreamWaitEvent(st, aux->join, 0) != hipSuccess)
+    (void)hipStreamSynchronize(aux->s2);  // the join failed: wait on the host instead
 }
 
 // k_big_assemble's launch shape: per tile position ceil(nchl / WPB) workgroups of WPB
