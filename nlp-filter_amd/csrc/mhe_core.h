@@ -1372,6 +1372,9 @@ __device__ __forceinline__ bool factor_forward(const GnArgs& a, const SmemLayout
 #ifndef MHE_SB_WEIGHTED
 #define MHE_SB_WEIGHTED 0  // A/B: 7:6 weighted tile shares (factorization -10 %, build / backward slower: -3 % overall)
 #endif
+#ifndef MHE_GN_SB
+#define MHE_GN_SB 1  // 0: no small-batch factorization (A/B builds only: the round-4 small-batch instance)
+#endif
 constexpr int SB_WORKERS = 6;
 // Waves w and w + 4 share a SIMD, and the older one (1, 2, 3) wins the issue arbitration
 // of every pair, so with equal shares the younger one (5, 6, 7) finished an interval
@@ -2461,7 +2464,7 @@ int launch_gn(const mhe_dims* dm, GnArgs& a, int batch, int mode, hipStream_t st
     // a batch that gives each CU at most one trajectory runs the small-batch instance:
     // 256 VGPRs (no two-workgroups-per-CU register cap) and factor_forward_sb (C2 strong
     // scaling at 4-8 GPUs: 256 / 128 per GPU)
-    const bool sb = mode == MODE_SOLVE && !bounded && !huber && batch <= device_cus(st) &&
+    const bool sb = MHE_GN_SB && mode == MODE_SOLVE && !bounded && !huber && batch <= device_cus(st) &&
                     smem_bytes(dm, a.NT, false, true) + g_opt_smem_pad <= REG_LDS_LIMIT;
     const int smem = smem_bytes(dm, a.NT, bounded, sb) + g_opt_smem_pad;  // pad: mhe_set_option, occupancy A/B only
     if (smem > REG_LDS_LIMIT) return MHE_ERR_UNSUPPORTED;
