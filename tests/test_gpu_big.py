@@ -168,3 +168,28 @@ def test_left_and_right_looking_factorizations_agree(cfg):
     assert (out["1"][3] == out["0"][3]).all() and (out["1"][2] == out["0"][2]).all()
     print(f"{cfg}: left- vs right-looking max|dX| = {np.abs(Xa - Xb).max():.3e}")
     assert np.array_equal(Xa, Xb) and np.array_equal(out["1"][1], out["0"][1])
+
+
+def test_split_factorization_is_batch_invariant():
+    """C4 (NT = 188 >= 128 tile columns) runs the split factorization: per block column a
+    diagonal stage and k_big_rows, one workgroup per 8 rows of one trajectory; a batch that
+    is a multiple of 8 is remapped so a trajectory's row groups share an XCD.  A batch of 8
+    (remapped) agrees bitwise with the right-looking one-launch kernel on the same batch and
+    with trajectory 5 solved alone (batch 1: no remap, other workgroup ids)."""
+    w = configs.make_c4(B=8)
+    s = solver.from_workload(w)
+    assert s.large_system
+    split = _np(s.solve(w.X_init, w.U, w.Y, w.PAR, max_iter=2, tol=0.0))
+    torch.cuda.synchronize()
+    try:
+        assert s.lib.mhe_set_option(_lib.OPT_BIG_RIGHT_LOOKING, 1) >= 0
+        mono = _np(s.solve(w.X_init, w.U, w.Y, w.PAR, max_iter=2, tol=0.0))
+        torch.cuda.synchronize()
+    finally:
+        s.lib.mhe_set_option(_lib.OPT_BIG_RIGHT_LOOKING, 0)
+    one = _np(s.solve(w.X_init[5:6], w.U, w.Y[5:6], w.PAR, max_iter=2, tol=0.0))
+    assert (split[3] == split[3][0]).all()
+    for a, b in zip(split, mono):
+        assert np.array_equal(a, b)
+    for a, b in zip(one, split):
+        assert np.array_equal(a, b[5:6])
