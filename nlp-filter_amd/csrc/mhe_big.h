@@ -832,6 +832,9 @@ constexpr int BIG_WIDE_NT = MHE_BIG_WIDE_NT;
 #ifndef MHE_BIG_TWO_STREAMS
 #define MHE_BIG_TWO_STREAMS 0  // split factorization: the batch's two halves on two streams (C3 +1.4 %, C4 +0.8 %, C5 0 vs one stream)
 #endif
+#ifndef MHE_BIG_DIAG_REG
+#define MHE_BIG_DIAG_REG 1  // split diagonal stage: its rows' left-looking update register-resident (as k_big_rows)
+#endif
 #ifndef MHE_BIG_ROWS_KC
 #define MHE_BIG_ROWS_KC 4  // k_big_rows: k tiles per staged slab
 #endif
@@ -908,7 +911,65 @@ __device__ __forceinline__ void big_diag_block(const BigArgs& a, int k0, int ken
   double* UN = sm + DTS + BIG_NW * 16 + 16 + 2;
   double* LJ = UN + UNITS;
   const int NT = a.NT;
-  if constexpr (LL) {
+  if constexpr (LL && SPLITROWS && MHE_BIG_DIAG_REG) {
+    // ---- split form: the left-looking update of the block's own <= 8 rows, one row per
+    // wave with its (up to 8) block-column tiles as accumulators, the kb x 4 slab of L_Jk
+    // staged by LDS-DMA and shared by the 8 rows -- as k_big_rows, but in the tiles' own
+    // orientation (the diagonal block below reads them from H).  Branch-free: tiles past
+    // the row's diagonal and waves without a row compute on clamped tiles, stores only.
+    // Same operations and order per element as the pass below.
+    constexpr int KC = 4;
+    const int kb = kend - k0;
+    if (k0 > 0 && !(MHE_BIG_KO & 1)) {
+      const int wv = __builtin_amdgcn_readfirstlane(wave);
+      const int I = k0 + wv;
+      const bool act = I < kend;
+      const int Ic = act ? I : kend - 1, jlast = Ic - k0;
+      d4 acc[BIG_KB];
+#pragma unroll
+      for (int jj = 0; jj < BIG_KB; ++jj) {
+        const double* C = H + (size_t)big_tile_index(Ic, k0 + min(jj, jlast), NT) * 256;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[jj][r] = C[64 * r + lane];
+      }
+      for (int kc = 0; kc < k0; kc += KC) {
+        __syncthreads();  // the previous slab is consumed
+        stage_slab_lds(LJ, H, k0, kb, kc, KC, NT);  // L_Jk, J = k0 + jj, k = kc + kk
+        __syncthreads();
+        double an[4];
+        const double* L0 = H + (size_t)big_tile_index(Ic, kc, NT) * 256;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) an[r] = L0[64 * r + lane];
+#pragma unroll
+        for (int kk = 0; kk < KC; ++kk) {
+          double av[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) av[r] = an[r];  // negated by the MFMA
+          if (kk + 1 < KC) {
+            const double* Ln = H + (size_t)big_tile_index(Ic, kc + kk + 1, NT) * 256;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) an[r] = Ln[64 * r + lane];
+          }
+#pragma unroll
+          for (int jj = 0; jj < BIG_KB; ++jj) {
+            const double* Bt = LJ + (min(jj, jlast) * KC + kk) * 256;
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              acc[jj] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[r], Bt[64 * r + lane], acc[jj], 0, 0, MFMA_NEG_A);
+          }
+        }
+      }
+#pragma unroll
+      for (int jj = 0; jj < BIG_KB; ++jj) {
+        if (act && jj <= jlast) {
+          double* C = H + (size_t)big_tile_index(I, k0 + jj, NT) * 256;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) C[64 * r + lane] = acc[jj][r];
+        }
+      }
+    }
+    __syncthreads();  // the block column's tiles are up to date; LJ is free for LB / LTs
+  } else if constexpr (LL) {
     // ---- left-looking update of block column k0 by all previous columns: a wave
     // takes LLR rows (g0 + wave + 8 q), so one staged slab serves 8 LLR rows
     constexpr int LLR = BIG_JB == 8 ? MHE_BIG_LLR8 : 2;

@@ -2509,7 +2509,7 @@ struct BigCholPlan {
   void (*mono)(BigArgs, int);
   void (*diag)(BigArgs, int);
   void (*bwd)(BigArgs, int);
-  int smem, smem_rows;
+  int smem, smem_rows, smem_diag;
   bool split;
 };
 inline int big_chol_plan(const BigArgs& A, BigCholPlan& p) {
@@ -2519,11 +2519,17 @@ inline int big_chol_plan(const BigArgs& A, BigCholPlan& p) {
   const bool ll = g_opt_big_right_looking == 0;
   p.split = ll && (MHE_BIG_SPLIT == 1 || (MHE_BIG_SPLIT == 2 && wide));
   p.mono = wide ? (ll ? k_big_chol<8, true> : k_big_chol<8>) : (ll ? k_big_chol<4, true> : k_big_chol<4>);
-  p.diag = wide ? k_big_chol<8, true, 1> : k_big_chol<4, true, 1>;
+  // the split diagonal stage stages a kb x 4 slab at any width (MHE_BIG_DIAG_REG): the
+  // 4-wide instance's LDS, two workgroups per CU
+  const bool d4w = MHE_BIG_DIAG_REG != 0;
+  p.diag = wide && !d4w ? k_big_chol<8, true, 1> : k_big_chol<4, true, 1>;
+  p.smem_diag = big_chol_lds(wide && !d4w ? 8 : 4) * (int)sizeof(double);
   p.bwd = wide ? k_big_chol<8, true, 2> : k_big_chol<4, true, 2>;
-  for (auto f : {p.mono, p.diag, p.bwd})
+  for (auto f : {p.mono, p.bwd})
     if (hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, p.smem) != hipSuccess)
       return -1;
+  if (hipFuncSetAttribute((const void*)p.diag, hipFuncAttributeMaxDynamicSharedMemorySize, p.smem_diag) != hipSuccess)
+    return -1;
   if (hipFuncSetAttribute((const void*)k_big_rows<>, hipFuncAttributeMaxDynamicSharedMemorySize, p.smem_rows) !=
       hipSuccess)
     return -1;
@@ -2534,7 +2540,7 @@ inline void launch_big_split(const BigCholPlan& p, BigArgs A, int boff, int nb, 
   A.ws += (size_t)boff * A.ws_stride;  // the stages index trajectories by workgroup only
   A.state += boff;
   for (int k0 = 0; k0 < A.NT; k0 += BIG_KB) {
-    hipLaunchKernelGGL(p.diag, dim3(nb), dim3(BIG_NTHREADS), p.smem, st, A, k0);
+    hipLaunchKernelGGL(p.diag, dim3(nb), dim3(BIG_NTHREADS), p.smem_diag, st, A, k0);
     const int kend = k0 + BIG_KB < A.NT ? k0 + BIG_KB : A.NT;
     if (kend < A.NT)
       hipLaunchKernelGGL(k_big_rows<>, dim3((A.NT - kend + BIG_NW - 1) / BIG_NW, nb), dim3(BIG_NTHREADS),
