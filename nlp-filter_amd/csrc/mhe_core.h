@@ -24,6 +24,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <math.h>
+#include <mutex>
 #include <stdint.h>
 #include <stdlib.h>
 
@@ -2535,12 +2536,15 @@ inline int big_chol_plan(const BigArgs& A, BigCholPlan& p) {
     return -1;
   return 0;
 }
-// One half of the batch through the split stages (trajectories boff .. boff + nb - 1).
-inline void launch_big_split(const BigCholPlan& p, BigArgs A, int boff, int nb, hipStream_t st) {
+// One half of the batch through the split stages (trajectories boff .. boff + nb - 1);
+// after_first (two-stream form): recorded on st after the first diagonal stage.
+inline void launch_big_split(const BigCholPlan& p, BigArgs A, int boff, int nb, hipStream_t st,
+                             hipEvent_t after_first = nullptr) {
   A.ws += (size_t)boff * A.ws_stride;  // the stages index trajectories by workgroup only
   A.state += boff;
   for (int k0 = 0; k0 < A.NT; k0 += BIG_KB) {
     hipLaunchKernelGGL(p.diag, dim3(nb), dim3(BIG_NTHREADS), p.smem_diag, st, A, k0);
+    if (k0 == 0 && after_first) (void)hipEventRecord(after_first, st);
     const int kend = k0 + BIG_KB < A.NT ? k0 + BIG_KB : A.NT;
     if (kend < A.NT)
       hipLaunchKernelGGL(k_big_rows<>, dim3((A.NT - kend + BIG_NW - 1) / BIG_NW, nb), dim3(BIG_NTHREADS),
@@ -2558,8 +2562,10 @@ struct BigAux {
 inline BigAux* big_aux() {
   static BigAux aux[16];
   static int made[16] = {0};
+  static std::mutex mu;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return nullptr;
+  std::lock_guard<std::mutex> lock(mu);
   if (!made[dev]) {
     if (hipStreamCreateWithFlags(&aux[dev].s2, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&aux[dev].fork, hipEventDisableTiming) != hipSuccess ||
@@ -2585,11 +2591,12 @@ inline void launch_big_factor(const BigCholPlan& p, const BigArgs& A, int batch,
     return;
   }
   const int h = ((batch / 2) + 7) & ~7;  // a multiple of 8 (k_big_rows' XCD grouping)
-  if (hipEventRecord(aux->fork, st) != hipSuccess || hipStreamWaitEvent(aux->s2, aux->fork, 0) != hipSuccess) {
-    launch_big_split(p, A, 0, batch, st);
-    return;
+  // the second half starts one diagonal stage behind the first, so that the halves'
+  // latency-bound diagonal stages alternate with the other half's row launches
+  launch_big_split(p, A, 0, h, st, aux->fork);
+  if (hipStreamWaitEvent(aux->s2, aux->fork, 0) != hipSuccess) {
+    (void)hipStreamSynchronize(st);
   }
-  launch_big_split(p, A, 0, h, st);
   launch_big_split(p, A, h, batch - h, aux->s2);
   if (hipEventRecord(aux->join, aux->s2) != hipSuccess || hipStreamWaitEvent(st, aux->join, 0) != hipSuccess)
     (void)hipStreamSynchronize(aux->s2);  // the join failed: wait on the host instead
