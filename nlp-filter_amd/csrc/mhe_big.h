@@ -1430,27 +1430,14 @@ __global__ __launch_bounds__(BIG_NTHREADS, BIG_JB == 8 ? 2 : 4) void k_big_chol(
 //            the slab and LB tiles every group of the trajectory stages come from that L2.
 // LDS: two slabs, then (same region) the block's in-block L tiles LB and L_kk^-T.
 __host__ __device__ constexpr int big_rows_lds() { return BIG_LB_TILES * 256 + BIG_KB * DTS; }  // doubles
-template <int KC = MHE_BIG_ROWS_KC, bool DB = MHE_BIG_ROWS_DB != 0>
-__global__ __launch_bounds__(BIG_NTHREADS, 4) void k_big_rows(BigArgs a, int k0) {
+// One group of BIG_NW rows below block column k0 (rows kend + 8 grp + wave): the body of
+// k_big_rows.  sm: the LDS region of the slabs, LB and LTs (big_rows_lds() doubles).
+template <int KC, bool DB>
+__device__ __forceinline__ void big_rows_group(double* H, const double* LTg, double* BV, const double* YV,
+                                               double* sm, int NT, int k0, int grp) {
   static_assert((DB ? 2 : 1) * BIG_KB * KC * 256 <= big_rows_lds(), "the slabs fit the LDS region");
-  const int G = gridDim.x;
-  int b = blockIdx.y, grp = blockIdx.x;
-  if (MHE_BIG_ROWS_XCD && (gridDim.y & 7) == 0) {
-    const int L = blockIdx.x + G * blockIdx.y, x = L & 7, j = L >> 3;
-    b = 8 * (j / G) + x;
-    grp = j - G * (j / G);
-  }
-  if (a.state[b] != BIG_RUNNING) return;
-  const BigWs WL = big_ws_layout(a.P, a.M, a.n, a.NT, a.nz, a.nc);
-  double* ws = a.ws + (size_t)b * a.ws_stride;
-  double* H = ws + WL.H;
-  const double* LTg = ws + WL.LT;
-  double* BV = ws + WL.BV;
-  const double* YV = ws + WL.YV;
-  extern __shared__ __attribute__((aligned(16))) double sm[];
   double* LB = sm;
   double* LTs = sm + BIG_LB_TILES * 256;
-  const int NT = a.NT;
   const int kend = min(k0 + BIG_KB, NT), kb = kend - k0;
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = lane >> 4, c = lane & 15;
@@ -1553,6 +1540,22 @@ __global__ __launch_bounds__(BIG_NTHREADS, 4) void k_big_rows(BigArgs a, int k0)
       if (lane < 16) BV[16 * I + lane] -= s;
     }
   }
+}
+
+template <int KC = MHE_BIG_ROWS_KC, bool DB = MHE_BIG_ROWS_DB != 0>
+__global__ __launch_bounds__(BIG_NTHREADS, 4) void k_big_rows(BigArgs a, int k0) {
+  const int G = gridDim.x;
+  int b = blockIdx.y, grp = blockIdx.x;
+  if (MHE_BIG_ROWS_XCD && (gridDim.y & 7) == 0) {
+    const int L = blockIdx.x + G * blockIdx.y, x = L & 7, j = L >> 3;
+    b = 8 * (j / G) + x;
+    grp = j - G * (j / G);
+  }
+  if (a.state[b] != BIG_RUNNING) return;
+  const BigWs WL = big_ws_layout(a.P, a.M, a.n, a.NT, a.nz, a.nc);
+  double* ws = a.ws + (size_t)b * a.ws_stride;
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  big_rows_group<KC, DB>(ws + WL.H, ws + WL.LT, ws + WL.BV, ws + WL.YV, sm, a.NT, k0, grp);
 }
 
 // ------------------------------------------------------------ border (f4)
