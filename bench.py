@@ -47,6 +47,17 @@ def algorithmic_flops_per_traj_iter(P, n, M):
     return d ** 3 / 3.0 + 2.0 * d * d + 6.0 * d * (d + 1) / 2.0 + 4.0 * P * P * n + 4.0 * M * P * n
 
 
+def gn_kernel_name(B, dev):
+    """The k_gn instance launch_gn picks for this per-GPU batch (csrc/mhe_core.h): the
+    small-batch factorization when every trajectory has a CU of its own, else the
+    two-workgroups-per-CU instance."""
+    import torch
+    if B <= torch.cuda.get_device_properties(dev).multi_processor_count:
+        return ("mhe::k_gn<DynVanDerPol, MeasFullState<2>, SLOTS=13, MODE_SOLVE, HUBER=false, MINW=2, SB=true> "
+                "(small-batch factorization)")
+    return "mhe::k_gn<DynVanDerPol, MeasFullState<2>, SLOTS=10, MODE_SOLVE, HUBER=false>"
+
+
 def survey_flops_per_traj_iter(P, n, E, nnz_g):
     """SURVEY.md §8(d) algorithmic FLOPs per trajectory per GN iteration (the
     roofline's `achieved` basis): Cholesky d^3/3 + two triangular solves 2 d^2
@@ -229,7 +240,7 @@ def main():
                        "parallelism": f"dp{world} (independent trajectories; RCCL broadcast of constants only)"},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None,
-                         "kernel": "mhe::k_gn<DynVanDerPol, MeasFullState<2>, SLOTS=10, MODE_SOLVE, HUBER=false>",
+                         "kernel": gn_kernel_name(B, dev),
                          "kernel_ms": kern_ms,
                          "flops_per_launch": fl,
                          "flops_basis": "SURVEY.md 8(d): d^3/3 + 2d^2 + sum_e P^2 nnz(G_e) + 2P^2n^2 + 4Pn^3 "
