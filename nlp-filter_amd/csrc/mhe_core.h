@@ -2559,12 +2559,14 @@ struct BigAux {
   hipStream_t s2;
   hipEvent_t fork, join;
 };
-inline BigAux* big_aux() {
+inline BigAux* big_aux(hipStream_t st) {
   static BigAux aux[16];
   static int made[16] = {0};
   static std::mutex mu;
-  int dev = 0;
+  int dev = 0, sdev = -1;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return nullptr;
+  // the second stream is created on the current device: only when the launch stream is on it
+  if (hipStreamGetDevice(st, &sdev) != hipSuccess || sdev != dev) return nullptr;
   std::lock_guard<std::mutex> lock(mu);
   if (!made[dev]) {
     if (hipStreamCreateWithFlags(&aux[dev].s2, hipStreamNonBlocking) != hipSuccess ||
@@ -2585,7 +2587,7 @@ inline void launch_big_factor(const BigCholPlan& p, const BigArgs& A, int batch,
     hipLaunchKernelGGL(p.mono, dim3(batch), dim3(BIG_NTHREADS), p.smem, st, A, 0);
     return;
   }
-  BigAux* aux = MHE_BIG_TWO_STREAMS && batch >= 16 ? big_aux() : nullptr;
+  BigAux* aux = MHE_BIG_TWO_STREAMS && batch >= 16 ? big_aux(st) : nullptr;
   if (!aux) {
     launch_big_split(p, A, 0, batch, st);
     return;
