@@ -1,7 +1,8 @@
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
-for B in 128 256 512; do
-  timeout -k 10 300 python bench.py --global-batch $B --steps 20 --warmup 5 > gpurun_out/r05_bench_B$B.log 2>&1 || exit $?
-done
-timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu > gpurun_out/r05_bench_B1024_nocpu.log 2>&1 || exit $?
-for f in gpurun_out/r05_bench_B*.log; do python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[1], '%.4g' % d['value'], d['roofline']['kernel'], d['roofline'].get('traffic'))" $f; done
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+bash tools/reproduce.sh r05d suite close || exit $?
+B="python bench.py --global-batch 128 --steps 10 --warmup 2 --no-cpu"
+timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVE_CYCLES --output-format csv -d gpurun_out/pmc_r05_sb128 -o run -- $B > gpurun_out/pmc_r05_sb128.log 2>&1 || exit $?
+timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU --output-format csv -d gpurun_out/pmc2_r05_sb128 -o run -- $B > gpurun_out/pmc2_r05_sb128.log 2>&1 || exit $?
+ls gpurun_out/pmc_r05_sb128 gpurun_out/pmc2_r05_sb128
