@@ -146,6 +146,32 @@ def test_large_chol_solve_random_spd_and_non_spd():
     assert np.allclose(delta[0], -1.0) and np.isnan(delta[1:]).all()
 
 
+def test_large_chol_solve_wide_split_spd_and_non_spd():
+    """The wide-system factorization (C4 shape, NT = 188 tile columns: per block column a
+    diagonal-stage launch and a k_big_rows launch, then the solve launch): a random SPD
+    system against LAPACK, and a non-SPD pivot in a middle block column / a NaN in a late
+    one -- the diagonal stage that meets it stops the trajectory, the later launches skip
+    it, the others are unaffected."""
+    w = configs.make_c4(B=1)
+    s = solver.from_workload(w)
+    assert s.large_system and s.dp // 16 >= 128
+    rng = np.random.default_rng(12)
+    dp = s.dp
+    A = rng.normal(size=(dp, dp)) / np.sqrt(dp)
+    H1 = A @ A.T + np.eye(dp)
+    g1 = rng.normal(size=dp)
+    H = np.stack([H1, np.eye(dp), np.eye(dp)])
+    H[1, dp // 2, dp // 2] = -1.0
+    H[2, dp - 20, dp - 20] = np.nan
+    g = np.stack([g1, np.ones(dp), np.ones(dp)])
+    delta, status = _np(s.chol_solve(H, g))
+    assert status.tolist() == [0, 2, 2]
+    ref = -np.linalg.solve(H1, g1)
+    tl.check("wide random SPD solve", np.abs(delta[0] - ref).max(), 1e-10 * np.abs(ref).max())
+    assert _backward_error(H1, g1, delta[0]) <= 64 * EPS
+    assert np.isnan(delta[1:]).all()
+
+
 def test_constants_of_other_dims_refused_by_parity_entry_points():
     w = configs.make_c3(B=2, N=60)
     s = solver.from_workload(w)
