@@ -220,6 +220,8 @@ __device__ void big_nodes_sparse(const BigArgs& a, const BigConst& CL, const Big
   for (int k = threadIdx.x; k < a.P; k += BIG_NTHREADS) {
     double W[n], f[n], Fv[NNZ], uk[m > 0 ? m : 1];
     for (int c = 0; c < n; ++c) W[c] = 0.0;
+    constexpr int UJ = n <= 8 ? 8 : 2;  // loads in flight; n = 40 (C5) would spill at 8
+#pragma unroll UJ
     for (int j = 0; j < a.P; ++j) {
       const double dv = Dt[(size_t)j * a.P + k];
       for (int c = 0; c < n; ++c) W[c] += dv * X[j * n + c];
@@ -296,6 +298,7 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_resid(BigArgs a, int final
   for (int e = threadIdx.x; e < E; e += BIG_NTHREADS) {
     double xe[n];
     for (int c = 0; c < n; ++c) xe[c] = 0.0;
+    #pragma unroll 8
     for (int j = 0; j < a.P; ++j) {
       const double ph = PhiET[(size_t)j * Mr + e];
       for (int c = 0; c < n; ++c) xe[c] += ph * X[j * n + c];
@@ -309,6 +312,7 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_resid(BigArgs a, int final
   for (int k = threadIdx.x; k < a.P; k += BIG_NTHREADS) {
     double dx[n], xk[n], uk[m > 0 ? m : 1], f[n], F[n * n];
     for (int c = 0; c < n; ++c) dx[c] = 0.0;
+    #pragma unroll 8
     for (int j = 0; j < a.P; ++j) {
       const double dv = Dt[(size_t)j * a.P + k];
       for (int c = 0; c < n; ++c) dx[c] += dv * X[j * n + c];
@@ -472,8 +476,10 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_resid(BigArgs a, int final
     double gv = 0.0;
     if (j < a.P) {
       double s = 0.0;
+      #pragma unroll 8
       for (int k = 0; k < a.P; ++k) s += D[(size_t)k * a.P + j] * ws[WL.Vs + k * n + c];
       double o = 0.0;
+      #pragma unroll 8
       for (int e = 0; e < E; ++e) o += PhiE[(size_t)e * a.P + j] * ws[WL.GEe + e * n + c];
       gv = a.alpha * s - ws[WL.FtV + j * n + c] - o;
       if (a.has_prior && j == 0) {
@@ -1850,6 +1856,8 @@ __device__ double big_cost(const BigArgs& a, const double* X, int b, double* red
   for (int k = threadIdx.x; k < a.P; k += BIG_NTHREADS) {
     double dx[n], xk[n], uk[m > 0 ? m : 1], f[n];
     for (int c = 0; c < n; ++c) dx[c] = 0.0;
+    constexpr int UJ = n <= 8 ? 8 : 2;  // loads in flight; n = 40 (C5) would spill at 8
+#pragma unroll UJ
     for (int j = 0; j < a.P; ++j) {
       const double dv = Dt[(size_t)j * a.P + k];
       for (int c = 0; c < n; ++c) dx[c] += dv * X[j * n + c];
@@ -1883,6 +1891,8 @@ __device__ double big_cost(const BigArgs& a, const double* X, int b, double* red
   for (int e = threadIdx.x; e < E; e += BIG_NTHREADS) {
     double xe[NAX];
     for (int c = 0; c < NAX; ++c) xe[c] = 0.0;
+    constexpr int UJ = n <= 8 ? 8 : 2;  // loads in flight; n = 40 (C5) would spill at 8
+#pragma unroll UJ
     for (int j = 0; j < a.P; ++j) {
       const double ph = PhiET[(size_t)j * Mr + e];
       for (int c = 0; c < n; ++c) xe[c] += ph * X[j * n + c];
