@@ -47,15 +47,14 @@ def algorithmic_flops_per_traj_iter(P, n, M):
     return d ** 3 / 3.0 + 2.0 * d * d + 6.0 * d * (d + 1) / 2.0 + 4.0 * P * P * n + 4.0 * M * P * n
 
 
-def gn_kernel_name(B, dev):
-    """The k_gn instance launch_gn picks for this per-GPU batch (csrc/mhe_core.h): the
-    small-batch factorization when every trajectory has a CU of its own, else the
-    two-workgroups-per-CU instance."""
-    import torch
-    if B <= torch.cuda.get_device_properties(dev).multi_processor_count:
-        return ("mhe::k_gn<DynVanDerPol, MeasFullState<2>, SLOTS=13, MODE_SOLVE, HUBER=false, MINW=2, SB=true> "
-                "(small-batch factorization)")
-    return "mhe::k_gn<DynVanDerPol, MeasFullState<2>, SLOTS=10, MODE_SOLVE, HUBER=false>"
+def gn_kernel_name(s, B, stream):
+    """The k_gn instance the library's launch_gn selects for this solver and per-GPU
+    batch on this stream's device (mhe_solve_kernel_name: the same conditions as the
+    launch -- batch vs CUs, Huber, bounds, LDS fit)."""
+    import ctypes
+    buf = ctypes.create_string_buffer(256)
+    rc = s.lib.mhe_solve_kernel_name(s.dims, B, ctypes.c_void_p(stream.cuda_stream), buf, 256)
+    return buf.value.decode() if rc == 0 else f"unknown (rc {rc})"
 
 
 def survey_flops_per_traj_iter(P, n, E, nnz_g):
@@ -187,6 +186,12 @@ def main():
     dist.broadcast_(s.cbuf, src=0)
     if rank != 0:
         s.constants_ready()
+    # the line proves its rank count by collectives: every rank adds 1, and 1 more when its
+    # received constants carry rank 0's digest (the layout stamp and every byte after it)
+    ranks_seen, constants_ok_ranks = dist.verify_broadcast(s.cbuf, dev)
+    if ranks_seen != world or constants_ok_ranks != world:
+        raise SystemExit(f"rank {rank}: {ranks_seen} ranks seen, {constants_ok_ranks} with rank 0's constants "
+                         f"(WORLD_SIZE={world})")
     staged = s.prepare(w.X_init, w.U, w.Y)
     B = w.B
     outs = (torch.empty_like(staged[0]), torch.empty(B, dtype=torch.float64, device=dev),
@@ -225,6 +230,8 @@ def main():
             "value": value,
             "unit": "GN collocation-point updates/s",
             "n_gpus": world,
+            "ranks_seen": ranks_seen,              # all-reduce sum of 1 over the process group
+            "constants_ok_ranks": constants_ok_ranks,  # ranks whose broadcast constants match rank 0's
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": wall / args.steps * 1e3,
@@ -240,7 +247,7 @@ def main():
                        "parallelism": f"dp{world} (independent trajectories; RCCL broadcast of constants only)"},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None,
-                         "kernel": gn_kernel_name(B, dev),
+                         "kernel": gn_kernel_name(s, B, stream),
                          "kernel_ms": kern_ms,
                          "flops_per_launch": fl,
                          "flops_basis": "SURVEY.md 8(d): d^3/3 + 2d^2 + sum_e P^2 nnz(G_e) + 2P^2n^2 + 4Pn^3 "

@@ -111,7 +111,7 @@ extern "C" {
  * the size queries) unless it equals this build's sizeof -- a binding that
  * declares an older or truncated struct is refused before any later field is
  * read.  (mhe/_lib.py sets it in the ctypes constructors.) */
-#define MHE_ABI_VERSION 5
+#define MHE_ABI_VERSION 6
 
 typedef struct mhe_dims {
   int32_t struct_size;  /* = sizeof(mhe_dims)                                */
@@ -355,7 +355,7 @@ int mhe_chol_solve(const mhe_dims* dims, const void* const_buf, int32_t batch,
                    void* stream);
 
 /*
- * Both kernel-level parity entry points for EVERY path (ABI v5): on the register-
+ * Both kernel-level parity entry points for EVERY path (ABI v5+): on the register-
  * resident path they are mhe_assemble / mhe_chol_solve (workspace ignored, status
  * set to 0 by the assembly); on the large-system path (C3-C5, mhe_workspace_bytes > 0)
  * they run the solve's own kernels over a caller-owned workspace of
@@ -367,12 +367,18 @@ int mhe_chol_solve(const mhe_dims* dims, const void* const_buf, int32_t batch,
  *                      oracle's order; padding nodes last: identity block, zero coupling,
  *                      zero gradient), cost (B), status (B): 0, or
  *                      MHE_STATUS_BAD_CONSTANTS (outputs NaN).  The plain GN system
- *                      (bounds are a solve-time reduction); n_extra / n_eq > 0:
- *                      MHE_ERR_UNSUPPORTED (the bordered system is not exported).
+ *                      (bounds are a solve-time reduction).  n_extra / n_eq > 0: the
+ *                      bordered KKT system of mhe_assemble_kkt_ws below (Z = NULL, so
+ *                      n_extra > 0 returns MHE_ERR_NULL here: use the _kkt_ form).
  *   mhe_chol_solve_ws  H (lower triangle read, node-major as above) and g into the
  *                      tiles, k_big_chol (blocked Cholesky + both triangular solves),
  *                      delta = -H^-1 g (B,dp) node-major; status 0, MHE_STATUS_NOT_SPD
  *                      (non-positive or non-finite pivot; delta NaN) or BAD_CONSTANTS.
+ *                      n_extra / n_eq > 0 (ABI v6): H, g, delta are the KKT system of
+ *                      mhe_kkt_dim rows below, solved as every bordered GN step is
+ *                      (k_big_chol on the leading block, then k_big_border: the border
+ *                      columns through the factor, LDL^T of the Schur complement);
+ *                      delta = [dx; dz; lambda].
  */
 int mhe_assemble_ws(const mhe_dims* dims, const void* const_buf, int32_t batch,
                     const double* X, const double* U, int64_t u_bstride,
@@ -382,6 +388,34 @@ int mhe_assemble_ws(const mhe_dims* dims, const void* const_buf, int32_t batch,
 int mhe_chol_solve_ws(const mhe_dims* dims, const void* const_buf, int32_t batch,
                       const double* H, const double* g, double* delta, int32_t* status,
                       void* workspace, size_t workspace_bytes, void* stream);
+
+/*
+ * Kernel-level parity of the BORDERED system (ABI v6; SURVEY §8 f4: extra decision
+ * variables z, nlp/nlp.py:40-47 addVariables used by multi-receiver.py:73,99, and
+ * addEqConstraint rows, nlp/nlp.py:49-53 / gnss-multi-receiver.py:76-78).  Each
+ * bordered GN step solves, with K = n_extra + n_eq and dk = mhe_kkt_dim = dp + K,
+ *   [ H    H_xz  C^T ] [dx]     [ g_x       ]
+ *   [ H_zx H_zz  0   ] [dz] = - [ g_z       ]     (rows C v - r of the constraints)
+ *   [ C    0     0   ] [l ]     [ C v - r   ]
+ * mhe_assemble_kkt_ws exports that matrix (B,dk,dk) and right-hand side g (B,dk) at
+ * (X, Z): the leading dp x dp block is mhe_assemble_ws's node-major H, then the z rows,
+ * then the constraint rows, in the values the solve's own k_big_resid / k_big_border
+ * form (Z (B, n_extra) device array; NULL when n_extra == 0).  K = 0: exactly
+ * mhe_assemble_ws.  mhe_chol_solve_ws takes the same shapes back (see above).
+ */
+int32_t mhe_kkt_dim(const mhe_dims* dims);
+
+/* The kernel(s) a solve of `batch` trajectories on `stream` would run, as text into buf
+ * (len bytes, NUL-terminated): the register path's k_gn instance -- chosen by the same
+ * function as the launch (batch vs the stream device's CUs, Huber, bounds, LDS fit) --
+ * or the large-system path's kernel sequence.  Host-only query; launches nothing.
+ * (bench.py names the roofline record's kernel with it.) */
+int32_t mhe_solve_kernel_name(const mhe_dims* dims, int32_t batch, void* stream, char* buf, int32_t len);
+int mhe_assemble_kkt_ws(const mhe_dims* dims, const void* const_buf, int32_t batch,
+                        const double* X, const double* Z, const double* U, int64_t u_bstride,
+                        const double* Y, const double* PAR, int64_t par_bstride,
+                        const double* x0, double* H, double* g, double* cost, int32_t* status,
+                        void* workspace, size_t workspace_bytes, void* stream);
 
 /* ------------------------------------------------------------------------
  * Batched extended Kalman filter.

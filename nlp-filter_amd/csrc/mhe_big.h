@@ -59,7 +59,7 @@ __host__ __device__ inline BigConst big_const_layout(int P, int M, int n, int p,
 }
 
 struct BigWs {  // per-trajectory workspace offsets in doubles
-  size_t H, LT, BV, YV, XE, GEe, Ge, Es, FtE, Vs, FtV, GZe, HZZe, GZVe, BM, ZM, DZ, ACT, GV, NZ, LAM, total;
+  size_t H, LT, BV, YV, XE, GEe, Ge, Es, FtE, Vs, FtV, GZe, HZZe, GZVe, BM, ZM, DZ, ACT, GV, NZ, LAM, KS, total;
 };
 
 // nz extra variables, nc equality constraints (border of the KKT system)
@@ -93,6 +93,8 @@ __host__ __device__ inline BigWs big_ws_layout(int P, int M, int n, int NT, int 
                                                                  // overwrites BV with the forward solve)
   W.NZ = o;   o = al(o + 1);                                     // bounds: the cost's rounding level at X
   W.LAM = o;  o = al(o + (size_t)P * n);                         // Huber IRLS weights c_k lambda_ka
+  W.KS = o;   o = al(o + (size_t)K * K + 2 * K);                 // border: S (K x K), r, w of the last
+                                                                 // bordered step (kernel-level KKT parity)
   W.total = o;
   return W;
 }
@@ -134,6 +136,8 @@ struct BigArgs {
   long long rwstride;
   int huber;         // MHE_COST_HUBER: IRLS weights (k_big_resid), D^T diag(c lambda) D blocks (k_big_assemble)
   double huber_delta;
+  int border_import;  // k_big_border: the border B, S and r were imported into BM / ZM / KS
+                      // (mhe_chol_solve_ws on a KKT system) instead of formed at X
 };
 
 // measurement weights of trajectory b: the per-solve array when given, else the constants'
@@ -1338,9 +1342,15 @@ __global__ __launch_bounds__(BIG_NTHREADS, BIG_JB == 8 ? 2 : 4) void k_big_chol(
       __syncthreads();
     }
   }
-  if (*flag) {
-    if (threadIdx.x == 0) a.state[b] = MHE_STATUS_NOT_SPD;
-    return;
+  // SPLIT = 2 (the backward solve alone) runs no block column, so nothing orders thread
+  // 0's flag reset before the other waves' reads: it must not read the flag at all.  A
+  // non-SPD pivot was recorded in a.state by its diagonal stage (SPLIT = 1 launch), and
+  // such a trajectory returned at the state test above.
+  if constexpr (SPLIT != 2) {
+    if (*flag) {
+      if (threadIdx.x == 0) a.state[b] = MHE_STATUS_NOT_SPD;
+      return;
+    }
   }
   if constexpr (SPLIT == 1) return;  // the rows below and the solve are launches of their own
   // backward: delta_k = L_kk^-T (y_k - sum_{I>k} L_Ik^T delta_I), delta in place in YV.
@@ -1578,6 +1588,50 @@ __global__ __launch_bounds__(BIG_NTHREADS, 4) void k_big_rows(BigArgs a, int k0)
 // definite), so LDL^T without pivoting is stable; a z component no row depends on
 // (zero pivot with a zero row) is held fixed (dz = 0), the minimum-norm choice.
 // Dynamic LDS: K*K (Schur) + 2K (rhs / w, pivot column) doubles.
+// Border of the KKT system at the iterate, shared by k_big_border and the kernel-level
+// KKT export (mhe_assemble_kkt_ws), so both see the same values:
+//   column col < nz of B at component-major row (ca, j): (H_xz)_{(j,ca), col}
+//     = sum_e PhiE[e][j] GZe[e][ca][col]  (epoch order);
+//   column nz + k: the constraint row k's coefficients (+1 at eq[2k], -1 at eq[2k+1]);
+//   S[r][c] = sum_e HZZe[e][r][c] for r, c < nz (the constraint block 0);
+//   rhs r[i] = -g_z[i] = sum_e GZVe[e][i] (i < nz), -c(v) = -(v[a] - v[b] - r_k) else.
+__device__ __forceinline__ double big_border_col(const BigArgs& a, const double* ws, const BigWs& WL,
+                                                 const double* PhiE, const int* eq, int E, int n, int col, int ca,
+                                                 int j) {
+  constexpr int NZX = MHE_MAX_EXTRA;
+  double v = 0.0;
+  if (j < a.P && col < a.nz + a.nc) {
+    if (col < a.nz) {
+      for (int e = 0; e < E; ++e) v += PhiE[(size_t)e * a.P + j] * ws[WL.GZe + ((size_t)e * n + ca) * NZX + col];
+    } else {
+      const int fi = j * n + ca;  // node-major index of this row
+      if (eq[2 * (col - a.nz)] == fi) v += 1.0;
+      if (eq[2 * (col - a.nz) + 1] == fi) v -= 1.0;
+    }
+  }
+  return v;
+}
+__device__ __forceinline__ double big_border_s(const BigArgs& a, const double* ws, const BigWs& WL, int E, int r,
+                                               int c) {
+  constexpr int NZX = MHE_MAX_EXTRA;
+  double sv = 0.0;
+  if (r < a.nz && c < a.nz)
+    for (int e = 0; e < E; ++e) sv += ws[WL.HZZe + (size_t)e * NZX * NZX + r * NZX + c];
+  return sv;
+}
+__device__ __forceinline__ double big_border_rhs(const BigArgs& a, const double* ws, const BigWs& WL, const int* eq,
+                                                 const double* eqr, const double* X, int E, int r) {
+  constexpr int NZX = MHE_MAX_EXTRA;
+  double base = 0.0;
+  if (r < a.nz) {  // -g_z = sum H_z^T R e
+    for (int e = 0; e < E; ++e) base += ws[WL.GZVe + (size_t)e * NZX + r];
+  } else {  // -c(v)
+    const int ia = eq[2 * (r - a.nz)], ib = eq[2 * (r - a.nz) + 1];
+    base = -(X[ia] - (ib >= 0 ? X[ib] : 0.0) - eqr[r - a.nz]);
+  }
+  return base;
+}
+
 template <int n, int p>
 __global__ __launch_bounds__(BIG_NTHREADS) void k_big_border(BigArgs a) {
   constexpr int NZX = MHE_MAX_EXTRA;
@@ -1605,23 +1659,17 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_border(BigArgs a) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 
   // (1) border columns, component-major rows r = c*Pp + j (padding rows 0);
-  //     ZM columns K..KP-1 are zero (inert panel columns)
-  for (int t = threadIdx.x; t < KP * dp; t += BIG_NTHREADS) {
-    const int col = t / dp, r = t % dp, ca = r / Pp, j = r % Pp;
-    double v = 0.0;
-    if (col < K && j < a.P) {
-      if (col < nz) {
-        for (int e = 0; e < E; ++e) v += PhiE[(size_t)e * a.P + j] * ws[WL.GZe + ((size_t)e * n + ca) * NZX + col];
-      } else {
-        const int fi = j * n + ca;  // node-major index of this row
-        if (eq[2 * (col - nz)] == fi) v += 1.0;
-        if (eq[2 * (col - nz) + 1] == fi) v -= 1.0;
-      }
+  //     ZM columns K..KP-1 are zero (inert panel columns).  Imported (KKT parity): BM and
+  //     ZM hold the caller's columns already.
+  if (!a.border_import) {
+    for (int t = threadIdx.x; t < KP * dp; t += BIG_NTHREADS) {
+      const int col = t / dp, r = t % dp, ca = r / Pp, j = r % Pp;
+      const double v = big_border_col(a, ws, WL, PhiE, eq, E, n, col, ca, j);
+      if (col < K) BM[(size_t)col * dp + r] = v;
+      ZM[(size_t)col * dp + r] = v;
     }
-    if (col < K) BM[(size_t)col * dp + r] = v;
-    ZM[(size_t)col * dp + r] = v;
+    __syncthreads();
   }
-  __syncthreads();
 
   // (2) Z = H^-1 B in place in ZM, one 16-column panel at a time.  MFMA operand
   //     layout as in k_big_chol: A[i = l&15][m = 4r + (l>>4)], B[m][j = l&15],
@@ -1706,20 +1754,12 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_border(BigArgs a) {
     for (int i = lane; i < dp; i += 64) s += x[i] * y[i];
     s = wave_sum(s);
     if (lane == 0) {
+      const double* KS = ws + WL.KS;  // imported S (K x K) and r (K)
       if (isr) {
-        double base;
-        if (r < nz) {  // -g_z = sum H_z^T R e
-          base = 0.0;
-          for (int e = 0; e < E; ++e) base += ws[WL.GZVe + (size_t)e * NZX + r];
-        } else {       // -c(v)
-          const int ia = eq[2 * (r - nz)], ib = eq[2 * (r - nz) + 1];
-          base = -(X[ia] - (ib >= 0 ? X[ib] : 0.0) - eqr[r - nz]);
-        }
+        const double base = a.border_import ? KS[K * K + r] : big_border_rhs(a, ws, WL, eq, eqr, X, E, r);
         rw[r] = base - s;
       } else {
-        double sv = 0.0;
-        if (r < nz && c < nz)
-          for (int e = 0; e < E; ++e) sv += ws[WL.HZZe + (size_t)e * NZX * NZX + r * NZX + c];
+        const double sv = a.border_import ? KS[r * K + c] : big_border_s(a, ws, WL, E, r, c);
         Ms[r * K + c] = sv - s;
       }
     }
@@ -1763,6 +1803,7 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_border(BigArgs a) {
     YV[i] = s;
   }
   if (threadIdx.x < NZX) ws[WL.DZ + threadIdx.x] = threadIdx.x < nz ? rw[threadIdx.x] : 0.0;
+  for (int i = threadIdx.x; i < K; i += BIG_NTHREADS) ws[WL.KS + K * K + K + i] = rw[i];  // w = [dz; lambda]
   if (a.lam)
     for (int i = threadIdx.x; i < nc; i += BIG_NTHREADS) a.lam[(size_t)b * nc + i] = rw[nz + i];
 }

@@ -2455,19 +2455,34 @@ inline int device_cus(hipStream_t st) {
   return c;
 }
 
+// Which k_gn instance a register-path launch runs (launch_gn, and mhe_solve_kernel_name
+// for the records that name it): a function of the dims, the mode and the batch against
+// the launch stream's CU count only.
+struct GnChoice {
+  bool bounded, huber, sb;
+  int smem;
+};
+inline GnChoice gn_choice(const mhe_dims* dm, int NT, int batch, int mode, hipStream_t st) {
+  GnChoice c;
+  c.bounded = mode == MODE_SOLVE && dm->n_bounds > 0;
+  c.huber = dm->dyn_cost == MHE_COST_HUBER;
+  // a batch that gives each CU at most one trajectory runs the small-batch instance:
+  // 256 VGPRs (no two-workgroups-per-CU register cap) and factor_forward_sb (C2 strong
+  // scaling at 4-8 GPUs: 256 / 128 per GPU)
+  c.sb = MHE_GN_SB && mode == MODE_SOLVE && !c.bounded && !c.huber && batch <= device_cus(st) &&
+         smem_bytes(dm, NT, false, true) + g_opt_smem_pad <= REG_LDS_LIMIT;
+  c.smem = smem_bytes(dm, NT, c.bounded, c.sb) + g_opt_smem_pad;  // pad: mhe_set_option, occupancy A/B only
+  return c;
+}
+
 template <class DYN, class MEAS>
 int launch_gn(const mhe_dims* dm, GnArgs& a, int batch, int mode, hipStream_t st) {
   if constexpr (MEAS::MIXED) {
     return MHE_ERR_UNSUPPORTED;  // mixed rows: large-system path only
   } else {
-    const bool bounded = mode == MODE_SOLVE && dm->n_bounds > 0;
-    const bool huber = dm->dyn_cost == MHE_COST_HUBER;
-    // a batch that gives each CU at most one trajectory runs the small-batch instance:
-    // 256 VGPRs (no two-workgroups-per-CU register cap) and factor_forward_sb (C2 strong
-    // scaling at 4-8 GPUs: 256 / 128 per GPU)
-    const bool sb = MHE_GN_SB && mode == MODE_SOLVE && !bounded && !huber && batch <= device_cus(st) &&
-                    smem_bytes(dm, a.NT, false, true) + g_opt_smem_pad <= REG_LDS_LIMIT;
-    const int smem = smem_bytes(dm, a.NT, bounded, sb) + g_opt_smem_pad;  // pad: mhe_set_option, occupancy A/B only
+    const GnChoice ch = gn_choice(dm, a.NT, batch, mode, st);
+    const bool bounded = ch.bounded, huber = ch.huber, sb = ch.sb;
+    const int smem = ch.smem;
     if (smem > REG_LDS_LIMIT) return MHE_ERR_UNSUPPORTED;
     void (*kern)(GnArgs) = nullptr;
     if (bounded) kern = huber ? k_gn_bounded<DYN, MEAS, MAX_SLOTS, true> : k_gn_bounded<DYN, MEAS, MAX_SLOTS>;
@@ -2621,8 +2636,10 @@ inline BigAsmShape big_asm_shape(const BigArgs& A) {
 
 // Kernel-level parity stages of the large-system path (mhe_assemble_ws /
 // mhe_chol_solve_ws): BIG_STAGE_ASSEMBLE runs k_big_resid + k_big_assemble at A.X (H
-// tiles and BV = -g in the workspace, cost), BIG_STAGE_FACTOR runs k_big_chol on the
-// workspace's tiles and BV (delta in YV).  The state words are set by the caller.
+// tiles and BV = -g in the workspace, cost; with z also the per-epoch border sums),
+// BIG_STAGE_FACTOR runs k_big_chol on the workspace's tiles and BV (delta in YV) and,
+// for a bordered system, k_big_border on the border the caller imported (w in KS).
+// The state words are set by the caller.
 constexpr int BIG_STAGE_ASSEMBLE = 0, BIG_STAGE_FACTOR = 1;
 template <class DYN, class MEAS>
 int launch_big_stage(const mhe_dims* dm, BigArgs& A, int batch, int stage, hipStream_t st) {
@@ -2636,6 +2653,14 @@ int launch_big_stage(const mhe_dims* dm, BigArgs& A, int batch, int stage, hipSt
     BigCholPlan cp;
     if (big_chol_plan(A, cp) < 0) return MHE_ERR_HIP;
     launch_big_factor(cp, A, batch, st);
+    const int K = A.nz + A.nc;  // the bordered (KKT) step through the factor, as the solve's
+    if (K > 0) {
+      const int smem_b = (K * K + 2 * K) * (int)sizeof(double);
+      if (hipFuncSetAttribute((const void*)k_big_border<DYN::n, MEAS::p>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              smem_b) != hipSuccess)
+        return MHE_ERR_HIP;
+      hipLaunchKernelGGL((k_big_border<DYN::n, MEAS::p>), dim3(batch), dim3(BIG_NTHREADS), smem_b, st, A);
+    }
   }
   return hipGetLastError() == hipSuccess ? MHE_OK : MHE_ERR_HIP;
 }

@@ -19,6 +19,7 @@
 // tile registers.  Trajectories are independent: no inter-workgroup traffic.
 //
 // See DESIGN.md for the data layout, the roofline and the measurements.
+#include <cstdio>
 #include <string.h>
 
 #include "mhe_core.h"
@@ -357,8 +358,10 @@ __global__ void k_big_parity_finish(int batch, int* state) {
   if (b < batch && state[b] == BIG_RUNNING) state[b] = MHE_STATUS_CONVERGED;
 }
 
-// dense node-major H (full, both triangles) and g = -BV from the tiles; grid (x, batch)
-__global__ void k_big_export_hg(BigArgs a, int batch, double* Hout, double* gout) {
+// dense node-major H (full, both triangles) and g = -BV from the tiles into the leading
+// dp x dp block of a ld x ld matrix per trajectory (ld = dp, or dp + K for the KKT
+// system: k_big_export_border fills the rest); grid (x, batch)
+__global__ void k_big_export_hg(BigArgs a, int batch, int ld, double* Hout, double* gout) {
   const int b = blockIdx.y;
   const int dp = a.n * a.Pp;
   const BigWs WL = big_ws_layout(a.P, a.M, a.n, a.NT, a.nz, a.nc);
@@ -370,16 +373,43 @@ __global__ void k_big_export_hg(BigArgs a, int batch, double* Hout, double* gout
     const int R = big_cm(r, a.n, a.Pp), C = big_cm(c, a.n, a.Pp);
     const int hi = R >= C ? R : C, lo = R >= C ? C : R;
     const double v = ws[WL.H + (size_t)big_tile_index(hi >> 4, lo >> 4, a.NT) * 256 + (hi & 15) * 16 + (lo & 15)];
-    Hout[(size_t)b * nel + e] = ok ? v : NAN;
-    if (c == 0) gout[(size_t)b * dp + r] = ok ? -ws[WL.BV + R] : NAN;
+    Hout[(size_t)b * ld * ld + (size_t)r * ld + c] = ok ? v : NAN;
+    if (c == 0) gout[(size_t)b * ld + r] = ok ? -ws[WL.BV + R] : NAN;
   }
 }
 
-// the caller's dense node-major H (lower triangle read) and g into the tiles and BV = -g;
-// grid (lower tiles, batch), one thread per tile element
-__global__ void k_big_import_hg(BigArgs a, int batch, const double* Hin, const double* gin) {
+// The border of the KKT system at X (mhe_assemble_kkt_ws), in the rows / columns dp ..
+// dp + K - 1 after the dense H block:  [H  B; B^T  S] and g = [g_x; g_z; c(v) - r], the
+// values k_big_border forms for the solve (big_border_col / _s / _rhs); grid (K, batch)
+__global__ void k_big_export_border(BigArgs a, int batch, int p, double* Hout, double* gout) {
+  const int b = blockIdx.y, col = blockIdx.x;
+  const int n = a.n, dp = n * a.Pp, K = a.nz + a.nc, ld = dp + K;
+  const BigConst CL = big_const_layout(a.P, a.M, n, p, a.nc);
+  const BigWs WL = big_ws_layout(a.P, a.M, n, a.NT, a.nz, a.nc);
+  const double* ws = a.ws + (size_t)b * a.ws_stride;
+  const double* PhiE = (const double*)(a.cbuf + CL.PhiE);
+  const int* eq = (const int*)(a.cbuf + CL.eq);
+  const double* eqr = (const double*)(a.cbuf + CL.eqr);
+  const int E = a.M > 0 ? *(const int*)(a.cbuf + CL.ne) : 0;
+  const double* X = a.X + (size_t)b * a.P * n;
+  const bool ok = a.state[b] == BIG_RUNNING;
+  double* Hb = Hout + (size_t)b * ld * ld;
+  for (int r = threadIdx.x; r < dp; r += blockDim.x) {  // node-major row r = j n + ca
+    const int j = r / n, ca = r % n;
+    const double v = ok ? big_border_col(a, ws, WL, PhiE, eq, E, n, col, ca, j) : NAN;
+    Hb[(size_t)r * ld + dp + col] = v;
+    Hb[(size_t)(dp + col) * ld + r] = v;
+  }
+  for (int c = threadIdx.x; c < K; c += blockDim.x)
+    Hb[(size_t)(dp + col) * ld + dp + c] = ok ? big_border_s(a, ws, WL, E, col, c) : NAN;
+  if (threadIdx.x == 0) gout[(size_t)b * ld + dp + col] = ok ? -big_border_rhs(a, ws, WL, eq, eqr, X, E, col) : NAN;
+}
+
+// the caller's dense node-major H (lower triangle read; leading dp x dp block of a ld x ld
+// matrix) and g into the tiles and BV = -g; grid (lower tiles, batch), one thread per
+// tile element
+__global__ void k_big_import_hg(BigArgs a, int batch, int ld, const double* Hin, const double* gin) {
   const int b = blockIdx.y;
-  const int dp = a.n * a.Pp;
   const BigWs WL = big_ws_layout(a.P, a.M, a.n, a.NT, a.nz, a.nc);
   double* ws = a.ws + (size_t)b * a.ws_stride;
   int t = blockIdx.x, J = 0;  // tile t -> (I, J), I >= J, column-major over the lower triangle
@@ -392,19 +422,47 @@ __global__ void k_big_import_hg(BigArgs a, int batch, const double* Hin, const d
   const int R = 16 * I + tr, C = 16 * J + tc;  // component-major
   const int r = (R % a.Pp) * a.n + R / a.Pp, c = (C % a.Pp) * a.n + C / a.Pp;
   const int hi = r >= c ? r : c, lo = r >= c ? c : r;  // node-major, lower triangle
-  ws[WL.H + (size_t)blockIdx.x * 256 + threadIdx.x] = Hin[((size_t)b * dp + hi) * dp + lo];
-  if (I == J && tr == 0) ws[WL.BV + 16 * I + tc] = -gin[(size_t)b * dp + (C % a.Pp) * a.n + C / a.Pp];
+  ws[WL.H + (size_t)blockIdx.x * 256 + threadIdx.x] = Hin[((size_t)b * ld + hi) * ld + lo];
+  if (I == J && tr == 0) ws[WL.BV + 16 * I + tc] = -gin[(size_t)b * ld + (C % a.Pp) * a.n + C / a.Pp];
 }
 
-// delta (node-major) from YV (component-major)
-__global__ void k_big_export_delta(BigArgs a, int batch, double* delta) {
+// The caller's KKT border (rows dp .. dp + K - 1 of a ld = dp + K system, lower part read:
+// B^T and S) into the workspace k_big_border reads with border_import set: the columns
+// of B component-major in BM and ZM (the panel padding columns K .. KP - 1 zero), S and
+// r = -g_tail in KS; grid (KP, batch)
+__global__ void k_big_import_border(BigArgs a, int batch, const double* Hin, const double* gin) {
+  const int b = blockIdx.y, col = blockIdx.x;
+  const int n = a.n, dp = n * a.Pp, K = a.nz + a.nc, ld = dp + K;
+  const BigWs WL = big_ws_layout(a.P, a.M, n, a.NT, a.nz, a.nc);
+  double* ws = a.ws + (size_t)b * a.ws_stride;
+  const double* Hb = Hin + (size_t)b * ld * ld;
+  for (int R = threadIdx.x; R < dp; R += blockDim.x) {  // component-major row R = ca Pp + j
+    const int r = (R % a.Pp) * n + R / a.Pp;
+    const double v = col < K ? Hb[(size_t)(dp + col) * ld + r] : 0.0;
+    if (col < K) ws[WL.BM + (size_t)col * dp + R] = v;
+    ws[WL.ZM + (size_t)col * dp + R] = v;
+  }
+  if (col < K) {
+    for (int c = threadIdx.x; c < K; c += blockDim.x) {  // lower triangle of S, mirrored
+      const int hi = col >= c ? col : c, lo = col >= c ? c : col;
+      ws[WL.KS + (size_t)col * K + c] = Hb[(size_t)(dp + hi) * ld + dp + lo];
+    }
+    if (threadIdx.x == 0) ws[WL.KS + (size_t)K * K + col] = -gin[(size_t)b * ld + dp + col];
+  }
+}
+
+// delta (node-major) from YV (component-major), then the border unknowns w = [dz; lambda]
+// of the bordered step (K > 0); ld = dp + K per trajectory
+__global__ void k_big_export_delta(BigArgs a, int batch, int ld, double* delta) {
   const int dp = a.n * a.Pp;
   const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= (long long)batch * dp) return;
-  const int b = (int)(e / dp), r = (int)(e % dp);
+  if (e >= (long long)batch * ld) return;
+  const int b = (int)(e / ld), r = (int)(e % ld);
   const BigWs WL = big_ws_layout(a.P, a.M, a.n, a.NT, a.nz, a.nc);
   const double* ws = a.ws + (size_t)b * a.ws_stride;
-  delta[e] = a.state[b] == BIG_RUNNING ? ws[WL.YV + big_cm(r, a.n, a.Pp)] : NAN;
+  const int K = a.nz + a.nc;
+  const double v = r < dp ? ws[WL.YV + big_cm(r, a.n, a.Pp)] : ws[WL.KS + (size_t)K * K + K + (r - dp)];
+  delta[e] = a.state[b] == BIG_RUNNING ? v : NAN;
 }
 
 }  // namespace mhe
@@ -611,6 +669,42 @@ int mhe_assemble_ws(const mhe_dims* dims, const void* const_buf, int32_t batch, 
                     int64_t u_bstride, const double* Y, const double* PAR, int64_t par_bstride, const double* x0,
                     double* H, double* g, double* cost, int32_t* status, void* workspace, size_t workspace_bytes,
                     void* stream) {
+  return mhe_assemble_kkt_ws(dims, const_buf, batch, X, nullptr, U, u_bstride, Y, PAR, par_bstride, x0, H, g, cost,
+                             status, workspace, workspace_bytes, stream);
+}
+
+int32_t mhe_solve_kernel_name(const mhe_dims* dims, int32_t batch, void* stream, char* buf, int32_t len) {
+  int NT = 0;
+  const int rc = check_dims(dims, &NT);
+  if (rc != MHE_OK) return rc;
+  if (!buf || len <= 0) return MHE_ERR_NULL;
+  if (is_big(dims)) {
+    BigArgs A = make_big_args(dims, nullptr, NT, nullptr);
+    const bool wide = A.NT >= BIG_WIDE_NT, split = g_opt_big_right_looking == 0 && (MHE_BIG_SPLIT == 1 ||
+                                                                                      (MHE_BIG_SPLIT == 2 && wide));
+    snprintf(buf, len, "large-system path (dyn %d, meas %d, NT %d): k_big_resid, k_big_assemble, %s%s, k_big_%s",
+             dims->dyn_model, dims->meas_model, NT,
+             split ? "k_big_chol<8|4, LL, split stages> + k_big_rows" : (wide ? "k_big_chol<8" : "k_big_chol<4"),
+             split ? "" : (g_opt_big_right_looking ? ">" : ", LL>"), dims->n_bounds > 0 ? "linesearch" : "update");
+    return MHE_OK;
+  }
+  const GnChoice c = gn_choice(dims, NT, batch, MODE_SOLVE, (hipStream_t)stream);
+  if (c.smem > REG_LDS_LIMIT) return MHE_ERR_UNSUPPORTED;
+  snprintf(buf, len, "mhe::%s<dyn %d, meas %d, SLOTS=%d, MODE_SOLVE, HUBER=%d%s>%s", c.bounded ? "k_gn_bounded" : "k_gn",
+           dims->dyn_model, dims->meas_model, c.sb ? SB_SLOTS : MAX_SLOTS, c.huber ? 1 : 0,
+           c.sb ? ", MINW=2, SB=true" : "", c.sb ? " (small-batch factorization: batch <= CUs)" : " (two workgroups per CU)");
+  return MHE_OK;
+}
+
+int32_t mhe_kkt_dim(const mhe_dims* dims) {
+  const int32_t dp = mhe_padded_dim(dims);
+  return dp < 0 ? dp : dp + dims->n_extra + dims->n_eq;
+}
+
+int mhe_assemble_kkt_ws(const mhe_dims* dims, const void* const_buf, int32_t batch, const double* X, const double* Z,
+                        const double* U, int64_t u_bstride, const double* Y, const double* PAR, int64_t par_bstride,
+                        const double* x0, double* H, double* g, double* cost, int32_t* status, void* workspace,
+                        size_t workspace_bytes, void* stream) {
   int NT = 0;
   int rc = check_dims(dims, &NT);
   if (rc != MHE_OK) return rc;
@@ -621,10 +715,9 @@ int mhe_assemble_ws(const mhe_dims* dims, const void* const_buf, int32_t batch, 
       return MHE_ERR_HIP;
     return rc;
   }
-  if (dims->n_extra > 0 || dims->n_eq > 0) return MHE_ERR_UNSUPPORTED;  // the bordered KKT system is not exported
   if (batch <= 0) return batch == 0 ? MHE_OK : MHE_ERR_DIMS;
   if (!const_buf || !X || !H || !g || !cost || !status || (dims->M > 0 && !Y) || (dims->m > 0 && !U) ||
-      (dims->q > 0 && !PAR) || (dims->has_prior && !x0))
+      (dims->q > 0 && !PAR) || (dims->has_prior && !x0) || (dims->n_extra > 0 && !Z))
     return MHE_ERR_NULL;
   if (!workspace || workspace_bytes < mhe_workspace_bytes(dims, batch)) return MHE_ERR_NULL;
   const PairOps* ops = find_pair(dims);
@@ -633,15 +726,18 @@ int mhe_assemble_ws(const mhe_dims* dims, const void* const_buf, int32_t batch, 
   A.n_bounds = 0;  // the plain GN system: the projected method's reduction belongs to the solve
   A.U = U; A.ustride = u_bstride; A.Y = Y; A.PAR = PAR; A.pstride = par_bstride; A.x0 = x0;
   A.X = const_cast<double*>(X);  // read only by k_big_resid / k_big_assemble
+  A.Z = const_cast<double*>(Z);  // read only by k_big_resid
   A.cost = cost; A.state = status;
   const int nb = (batch + 255) / 256;
   hipLaunchKernelGGL(k_big_parity_init, dim3(nb), dim3(256), 0, st, A, batch);
   rc = ops->big_stage(dims, A, batch, BIG_STAGE_ASSEMBLE, st);
   if (rc != MHE_OK) return rc;
   const size_t dp = (size_t)A.n * A.Pp;
+  const int K = A.nz + A.nc;
   const size_t gx0 = (dp * dp + 255) / 256;
   const unsigned gx = (unsigned)(gx0 < 8192 ? gx0 : 8192);
-  hipLaunchKernelGGL(k_big_export_hg, dim3(gx, batch), dim3(256), 0, st, A, batch, H, g);
+  hipLaunchKernelGGL(k_big_export_hg, dim3(gx, batch), dim3(256), 0, st, A, batch, (int)dp + K, H, g);
+  if (K > 0) hipLaunchKernelGGL(k_big_export_border, dim3(K, batch), dim3(256), 0, st, A, batch, dims->p, H, g);
   hipLaunchKernelGGL(k_big_parity_finish, dim3(nb), dim3(256), 0, st, batch, status);
   return hipGetLastError() == hipSuccess ? MHE_OK : MHE_ERR_HIP;
 }
@@ -661,13 +757,17 @@ int mhe_chol_solve_ws(const mhe_dims* dims, const void* const_buf, int32_t batch
   BigArgs A = make_big_args(dims, const_buf, NT, workspace);
   A.n_bounds = 0;
   A.state = status;
+  A.border_import = 1;  // K > 0: the caller's border, not one formed at an iterate
+  A.lam = nullptr;
+  const int K = A.nz + A.nc, ld = A.n * A.Pp + K;
   const int nb = (batch + 255) / 256;
   hipLaunchKernelGGL(k_big_parity_init, dim3(nb), dim3(256), 0, st, A, batch);
-  hipLaunchKernelGGL(k_big_import_hg, dim3(NT * (NT + 1) / 2, batch), dim3(256), 0, st, A, batch, H, g);
+  hipLaunchKernelGGL(k_big_import_hg, dim3(NT * (NT + 1) / 2, batch), dim3(256), 0, st, A, batch, ld, H, g);
+  if (K > 0) hipLaunchKernelGGL(k_big_import_border, dim3((K + 15) / 16 * 16, batch), dim3(256), 0, st, A, batch, H, g);
   rc = ops->big_stage(dims, A, batch, BIG_STAGE_FACTOR, st);
   if (rc != MHE_OK) return rc;
-  const long long ne = (long long)batch * A.n * A.Pp;
-  hipLaunchKernelGGL(k_big_export_delta, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, st, A, batch, delta);
+  const long long ne = (long long)batch * ld;
+  hipLaunchKernelGGL(k_big_export_delta, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, st, A, batch, ld, delta);
   hipLaunchKernelGGL(k_big_parity_finish, dim3(nb), dim3(256), 0, st, batch, status);
   return hipGetLastError() == hipSuccess ? MHE_OK : MHE_ERR_HIP;
 }

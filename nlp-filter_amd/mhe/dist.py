@@ -43,6 +43,28 @@ def broadcast_(t, src=0):
     return t
 
 
+def _digest(t):
+    """Position-weighted checksum of a buffer's bytes (int64, on its device): two buffers
+    that differ in any byte or in byte order differ here (except by a ~2^-60 collision)."""
+    b = t.detach().reshape(-1).view(torch.uint8).to(torch.int64)
+    w = torch.arange(b.numel(), device=b.device, dtype=torch.int64) % 65521 + 1
+    return torch.stack([(b * w).sum(), b.sum(), torch.tensor(b.numel(), device=b.device)])
+
+
+def verify_broadcast(t, device, src=0):
+    """After broadcast_(t): (ranks_seen, ok_ranks) by collectives, not by the environment
+    -- ranks_seen = all-reduce sum of 1 over the process group, ok_ranks = the number of
+    ranks whose copy of ``t`` has rank ``src``'s digest.  One process: (1, 1)."""
+    d = _digest(t).to(device)
+    if not (dist.is_initialized() and dist.get_world_size() > 1):
+        return 1, 1
+    ref = d.clone()
+    dist.broadcast(ref, src=src)
+    cnt = torch.tensor([1.0, float(bool(torch.equal(ref, d)))], dtype=torch.float64, device=device)
+    dist.all_reduce(cnt, op=dist.ReduceOp.SUM)
+    return int(cnt[0].item()), int(cnt[1].item())
+
+
 def max_over_ranks(x, device):
     if not (dist.is_initialized() and dist.get_world_size() > 1):
         return float(x)

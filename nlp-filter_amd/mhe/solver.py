@@ -39,6 +39,14 @@ def _ptr(t):
     return None if t is None else ctypes_ptr(t)
 
 
+def _at(t, lo, per, itemsize=8):
+    """Pointer to trajectory ``lo`` of a batch-outermost tensor with ``per`` elements per
+    trajectory (per = 0: an input shared by the batch)."""
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr() + itemsize * lo * per)
+
+
 def ctypes_ptr(t):
     import ctypes
     return ctypes.c_void_p(t.data_ptr())
@@ -393,25 +401,44 @@ class BatchSolver:
             keep_alive(s, cur, X, U_t, Y_t, PAR_t, W, F, E, Hm)
         return W, F, E, Hm
 
-    def assemble(self, X, U, Y, PAR=None, x0=None, stream=None, status_out=False):
+    @property
+    def kkt_dim(self):
+        """Rows of the system assemble() / chol_solve() exchange: dp, plus n_extra + n_eq
+        border rows for a bordered (KKT) problem (mhe_kkt_dim)."""
+        return self.lib.mhe_kkt_dim(self.dims)
+
+    def assemble(self, X, U, Y, PAR=None, x0=None, stream=None, status_out=False, Z=None):
         """GN normal equations at X: H (B,dp,dp), g (B,dp), cost (B) -- dense, node-major
         (row j*n + c; padding nodes last) on both paths.  The large-system path runs the
-        solve's own k_big_resid + k_big_assemble over a workspace (mhe_assemble_ws) and
-        copies H out of their component-major tiles.  ``status_out``: also return the
+        solve's own k_big_resid + k_big_assemble over a workspace (mhe_assemble_kkt_ws) and
+        copies H out of their component-major tiles.  A bordered problem (n_extra / n_eq
+        > 0) returns the KKT system of kkt_dim rows instead (H_xz, H_zz, the constraint
+        rows; g = [g_x; g_z; C v - r]) at (X, Z).  ``status_out``: also return the
         per-trajectory status (0, or 4 = constants built for other dims)."""
         self._check_ready()
         with launch_stream(stream, self.device, (self._built,)) as (s, cur):
             X, B, U_t, ustr, Y_t, PAR_t, pstr, x0_t = self._inputs(X, U, Y, PAR, x0)
-            H = torch.empty((B, self.dp, self.dp), dtype=torch.float64, device=self.device)
-            g = torch.empty((B, self.dp), dtype=torch.float64, device=self.device)
+            Z_t = None
+            if self.n_extra:
+                Z_t = _dev(np.zeros((B, self.n_extra)) if Z is None else Z, self.device, (B, self.n_extra))
+            dk = self.kkt_dim
+            H = torch.empty((B, dk, dk), dtype=torch.float64, device=self.device)
+            g = torch.empty((B, dk), dtype=torch.float64, device=self.device)
             cost = torch.empty(B, dtype=torch.float64, device=self.device)
             status = torch.empty(B, dtype=torch.int32, device=self.device)
-            ws, nb = self._workspace(B, s)
-            rc = self.lib.mhe_assemble_ws(self.dims, _ptr(self.cbuf), B, _ptr(X), _ptr(U_t), ustr, _ptr(Y_t),
-                                          _ptr(PAR_t), pstr, _ptr(x0_t), _ptr(H), _ptr(g), _ptr(cost), _ptr(status),
-                                          _ptr(ws), nb, _handle(s))
-            _lib.check(rc, "mhe_assemble_ws")
-            keep_alive(s, cur, X, U_t, Y_t, PAR_t, x0_t, H, g, cost, status, ws)
+            # the large-system workspace is streamed in chunks like solve()'s (C5: 0.28 GB per
+            # trajectory), the outputs written in place at each chunk's offset
+            chunk = max(1, self._chunk(B, s))
+            ws, nb = self._workspace(chunk, s)
+            P, n, M = self.P, self.n, self.M
+            for lo in range(0, B, chunk):
+                c = min(chunk, B - lo)
+                rc = self.lib.mhe_assemble_kkt_ws(
+                    self.dims, _ptr(self.cbuf), c, _at(X, lo, P * n), _at(Z_t, lo, self.n_extra), _at(U_t, lo, ustr),
+                    ustr, _at(Y_t, lo, M * self.p), _at(PAR_t, lo, pstr), pstr, _at(x0_t, lo, n), _at(H, lo, dk * dk),
+                    _at(g, lo, dk), _at(cost, lo, 1), _at(status, lo, 1, 4), _ptr(ws), nb, _handle(s))
+                _lib.check(rc, "mhe_assemble_kkt_ws")
+            keep_alive(s, cur, X, Z_t, U_t, Y_t, PAR_t, x0_t, H, g, cost, status, ws)
         if status_out:
             return H, g, cost, status
         return H, g, cost
@@ -419,20 +446,26 @@ class BatchSolver:
     def chol_solve(self, H, g, stream=None):
         """delta = -H^{-1} g with the solver's own factorization (H: (B,dp,dp) SPD,
         node-major as ``assemble`` returns it; lower triangle read): the register-tiled
-        kernel, or on the large-system path k_big_chol over a workspace (mhe_chol_solve_ws)."""
+        kernel, or on the large-system path k_big_chol over a workspace (mhe_chol_solve_ws).
+        A bordered problem takes the KKT system of kkt_dim rows (``assemble``'s) and
+        returns delta = [dx; dz; lambda], solved as every bordered GN step (k_big_border)."""
         self._check_ready()
         with launch_stream(stream, self.device, (self._built,)) as (s, cur):
             H = _dev(H, self.device)
             g = _dev(g, self.device)
             B = H.shape[0]
-            if H.shape[1:] != (self.dp, self.dp) or g.shape != (B, self.dp):
-                raise ValueError(f"H must be (B,{self.dp},{self.dp}) and g (B,{self.dp})")
-            delta = torch.empty((B, self.dp), dtype=torch.float64, device=self.device)
+            dk = self.kkt_dim
+            if H.shape[1:] != (dk, dk) or g.shape != (B, dk):
+                raise ValueError(f"H must be (B,{dk},{dk}) and g (B,{dk})")
+            delta = torch.empty((B, dk), dtype=torch.float64, device=self.device)
             status = torch.empty(B, dtype=torch.int32, device=self.device)
-            ws, nb = self._workspace(B, s)
-            rc = self.lib.mhe_chol_solve_ws(self.dims, _ptr(self.cbuf), B, _ptr(H), _ptr(g), _ptr(delta),
-                                            _ptr(status), _ptr(ws), nb, _handle(s))
-            _lib.check(rc, "mhe_chol_solve_ws")
+            chunk = max(1, self._chunk(B, s))
+            ws, nb = self._workspace(chunk, s)
+            for lo in range(0, B, chunk):
+                c = min(chunk, B - lo)
+                rc = self.lib.mhe_chol_solve_ws(self.dims, _ptr(self.cbuf), c, _at(H, lo, dk * dk), _at(g, lo, dk),
+                                                _at(delta, lo, dk), _at(status, lo, 1, 4), _ptr(ws), nb, _handle(s))
+                _lib.check(rc, "mhe_chol_solve_ws")
             keep_alive(s, cur, H, g, delta, status, ws)
         return delta, status
 

@@ -35,7 +35,9 @@ work = w.B * w.P
 wall = dist.max_over_ranks(time.perf_counter() - t0, "cpu")
 total = dist.sum_over_ranks(work, "cpu")
 same = dist.sum_over_ranks(float(np.array_equal(D.numpy(), w.cpm.D)), "cpu")
+ranks_seen, ok_ranks = dist.verify_broadcast(D, "cpu")  # bench.py's self-proving rank count
 if rank == 0:
     print(json.dumps({"world": world, "total": total, "same": same, "wall": wall,
+                      "ranks_seen": ranks_seen, "constants_ok_ranks": ok_ranks,
                       "env": [os.environ["MASTER_ADDR"], os.environ["LOCAL_RANK"]]}))
 torch.distributed.destroy_process_group()

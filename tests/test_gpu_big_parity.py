@@ -172,6 +172,41 @@ def test_large_chol_solve_wide_split_spd_and_non_spd():
     assert np.isnan(delta[1:]).all()
 
 
+def test_wide_split_non_spd_neighbours_leave_healthy_deltas_bitwise():
+    """The split factorization's solve launch (k_big_chol SPLIT = 2) takes no flag from LDS
+    (a flag left by an earlier workgroup could stop some waves of a healthy
+    trajectory).  A batch alternating non-SPD and healthy SPD systems at the C4 shape: the
+    healthy deltas are bitwise those of the one-launch right-looking kernel on the healthy
+    systems alone, and the non-SPD ones are stopped."""
+    from mhe import _lib
+    w = configs.make_c4(B=1)
+    s = solver.from_workload(w)
+    assert s.large_system and s.dp // 16 >= 128
+    rng = np.random.default_rng(13)
+    dp, nh = s.dp, 4
+    Hh, gh = [], []
+    for _ in range(nh):
+        A = rng.normal(size=(dp, dp)) / np.sqrt(dp)
+        Hh.append(A @ A.T + np.eye(dp))
+        gh.append(rng.normal(size=dp))
+    H, g = [], []
+    for i in range(nh):
+        bad = np.eye(dp)
+        bad[(i * 397) % dp, (i * 397) % dp] = -1.0  # a non-SPD pivot in a different block column each
+        H += [bad, Hh[i]]
+        g += [np.ones(dp), gh[i]]
+    delta, status = _np(s.chol_solve(np.stack(H), np.stack(g)))
+    assert status.tolist() == [2, 0] * nh
+    try:
+        assert s.lib.mhe_set_option(_lib.OPT_BIG_RIGHT_LOOKING, 1) >= 0
+        ref, rst = _np(s.chol_solve(np.stack(Hh), np.stack(gh)))
+    finally:
+        s.lib.mhe_set_option(_lib.OPT_BIG_RIGHT_LOOKING, 0)
+    assert rst.tolist() == [0] * nh
+    assert np.array_equal(delta[1::2], ref)
+    assert np.isnan(delta[0::2]).all()
+
+
 def test_constants_of_other_dims_refused_by_parity_entry_points():
     w = configs.make_c3(B=2, N=60)
     s = solver.from_workload(w)

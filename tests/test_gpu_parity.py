@@ -190,3 +190,39 @@ def test_small_batch_instance_matches_full_occupancy_instance():
     small = [t.cpu().numpy() for t in s.solve(w.X_init[sub], w.U, w.Y[sub], max_iter=4, tol=0.0)]
     for a, b in zip(small, big):
         assert np.array_equal(a, b[sub])
+
+
+FULL_OCC = {
+    "c1": lambda B: configs.make_c1(B=B),                 # single_integrator pair (nlp/dynamics.py:4-7)
+    "c2_n20": lambda B: configs.make_c2(B=B, N=20),       # van der Pol pair
+    "gnss_small": lambda B: configs.make_gnss_small(B=B),  # pseudorange pair (nlp/measurements.py:56-70)
+}
+
+
+@pytest.mark.parametrize("name", sorted(FULL_OCC))
+def test_full_occupancy_instance_iterates_match_oracle(name):
+    """B = CUs + 8 runs the two-workgroups-per-CU instance k_gn<..., MAX_SLOTS, MODE_SOLVE>
+    (not the small-batch one the B <= 6 cases above select): 4 GN iterations at tol 0 of
+    every trajectory against the oracle, for each shipped model pair family."""
+    import ctypes
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    w = FULL_OCC[name](cus + 8)
+    s = solver.from_workload(w)
+    buf = ctypes.create_string_buffer(256)
+    st = torch.cuda.current_stream()
+    assert s.lib.mhe_solve_kernel_name(s.dims, w.B, ctypes.c_void_p(st.cuda_stream), buf, 256) == 0
+    print(buf.value.decode())
+    assert b"two workgroups per CU" in buf.value and b"SB=true" not in buf.value
+    pb = _problem(w)
+    it = 4
+    X, cost, iters, status = s.solve(w.X_init, w.U, w.Y, w.PAR, max_iter=it, tol=0.0)
+    run = lambda Y, pt=None: gn.gauss_newton(pb, w.X_init, _U(w), Y, _PAR(w), max_iter=it, tol=0.0, perturb=pt)  # noqa: E731
+    Xr, cr, ir, sr = run(w.Y)
+    fx, fc = tl.floor(lambda Y, pt: run(Y, pt)[:2], w.Y)
+    assert iters.cpu().numpy().tolist() == ir.tolist() == [it] * w.B
+    assert status.cpu().numpy().tolist() == sr.tolist() == [1] * w.B
+    tl.check(f"{name} B={w.B} X", np.abs(X.cpu().numpy() - Xr).max(), tl.bound(fx, Xr))
+    tl.check(f"{name} B={w.B} cost", np.abs(cost.cpu().numpy() - cr).max(), tl.FLOOR_MULT * fc + 1e-10 * np.abs(cr).max())
+    head = lambda a: None if a is None else (a[:6] if a.shape[0] > 1 else a)  # noqa: E731
+    sb = s.solve(w.X_init[:6], head(w.U), w.Y[:6], head(w.PAR), max_iter=it, tol=0.0)[0].cpu().numpy()
+    assert np.array_equal(sb, X.cpu().numpy()[:6])  # and bitwise what the small-batch instance gives

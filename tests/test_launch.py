@@ -29,6 +29,7 @@ def test_launch_two_gloo_ranks(monkeypatch, tmp_path):
     assert len(lines) == 1                       # rank 0 alone prints
     r = json.loads(lines[0])
     assert r["world"] == 2 and r["total"] == 8 * 21 and r["same"] == 2.0
+    assert r["ranks_seen"] == 2 and r["constants_ok_ranks"] == 2  # counted by collectives
     assert r["env"] == ["127.0.0.1", "0"]
 
 
