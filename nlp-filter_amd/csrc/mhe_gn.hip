@@ -400,8 +400,8 @@ __global__ void k_big_export_border(BigArgs a, int batch, int p, double* Hout, d
     Hb[(size_t)r * ld + dp + col] = v;
     Hb[(size_t)(dp + col) * ld + r] = v;
   }
-  for (int c = threadIdx.x; c < K; c += blockDim.x)
-    Hb[(size_t)(dp + col) * ld + dp + c] = ok ? big_border_s(a, ws, WL, E, col, c) : NAN;
+  for (int c = threadIdx.x; c < K; c += blockDim.x)  // S's lower triangle, as k_big_border's LDL^T reads it
+    Hb[(size_t)(dp + col) * ld + dp + c] = ok ? big_border_s(a, ws, WL, E, col >= c ? col : c, col >= c ? c : col) : NAN;
   if (threadIdx.x == 0) gout[(size_t)b * ld + dp + col] = ok ? -big_border_rhs(a, ws, WL, eq, eqr, X, E, col) : NAN;
 }
 
