@@ -1368,8 +1368,12 @@ __device__ __forceinline__ bool factor_forward(const GnArgs& a, const SmemLayout
 //            LDS (BAND), where backward_sb reads them (their owners' registers go stale)
 //   wave 4   y_{k-1} = L^-1 b_{k-1}, b_b -= U_{k-1,b}^T y_{k-1}  (b >= k)
 // PB (rows k - 1 and k of U) and HB are double-buffered, so one barrier per interval
-// orders every hand-off.  Bitwise-identical per trajectory whatever the batch position;
-// not bitwise equal to factor_forward (other summation order of the trailing updates).
+// orders every hand-off.  Every tile still receives its trailing updates in k order (the
+// deferral moves WHEN step k - 1's update is applied, not its order), so the factor --
+// and the iterates -- are bitwise those of factor_forward (the two-workgroups-per-CU
+// instance): tests/test_gpu_parity.py::test_small_batch_instance_matches_full_occupancy_instance
+// and ::test_full_occupancy_instance_iterates_match_oracle assert it, which is what keeps
+// results independent of the GPU count a strong split runs on.
 #ifndef MHE_SB_WEIGHTED
 #define MHE_SB_WEIGHTED 0  // A/B: 7:6 weighted tile shares (factorization -10 %, build / backward slower: -3 % overall)
 #endif
@@ -2569,7 +2573,11 @@ inline void launch_big_split(const BigCholPlan& p, BigArgs A, int boff, int nb, 
 }
 
 // The second stream and fork / join events of the two-stream split factorization, one set
-// per device, created on first use (nullptr: run on one stream).
+// per device, created on first use (nullptr: run on one stream).  SINGLE-CALLER ONLY: two
+// solves enqueued concurrently on different streams of one device would share the fork /
+// join events and could re-record them between another caller's record and wait.  The
+// option is an A/B knob (MHE_BIG_TWO_STREAMS, compiled off); it must stay off in any build
+// that serves concurrent callers.
 struct BigAux {
   hipStream_t s2;
   hipEvent_t fork, join;
