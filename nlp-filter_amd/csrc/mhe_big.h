@@ -845,6 +845,9 @@ constexpr int BIG_WIDE_NT = MHE_BIG_WIDE_NT;
 #ifndef MHE_BIG_DIAG_REG
 #define MHE_BIG_DIAG_REG 1  // split diagonal stage: its rows' left-looking update register-resident (as k_big_rows)
 #endif
+#ifndef MHE_BIG_DIAG_SKIP
+#define MHE_BIG_DIAG_SKIP 1  // split diagonal stage: skip the MFMAs of tiles past a row's diagonal, SIMD-balanced rows
+#endif
 #ifndef MHE_BIG_ROWS_KC
 #define MHE_BIG_ROWS_KC 4  // k_big_rows: k tiles per staged slab
 #endif
@@ -932,9 +935,15 @@ __device__ __forceinline__ void big_diag_block(const BigArgs& a, int k0, int ken
     const int kb = kend - k0;
     if (k0 > 0 && !(MHE_BIG_KO & 1)) {
       const int wv = __builtin_amdgcn_readfirstlane(wave);
-      const int I = k0 + wv;
+      // Row k0 + o needs only its o + 1 tiles up to the diagonal: the MFMAs of tiles past it
+      // (and every MFMA of a wave without a row) are skipped by wave-uniform branches
+      // (MHE_BIG_DIAG_SKIP), and the rows are dealt so that the two waves sharing a SIMD
+      // (w, w + 4) take rows o and 7 - o: 9 tiles per SIMD instead of up to 16.
+      const int o = (MHE_BIG_DIAG_SKIP && wv >= 4) ? 11 - wv : wv;
+      const int I = k0 + o;
       const bool act = I < kend;
       const int Ic = act ? I : kend - 1, jlast = Ic - k0;
+      const int jdo = MHE_BIG_DIAG_SKIP ? (act ? jlast : -1) : BIG_KB - 1;  // last tile computed
       d4 acc[BIG_KB];
 #pragma unroll
       for (int jj = 0; jj < BIG_KB; ++jj) {
@@ -962,10 +971,12 @@ __device__ __forceinline__ void big_diag_block(const BigArgs& a, int k0, int ken
           }
 #pragma unroll
           for (int jj = 0; jj < BIG_KB; ++jj) {
-            const double* Bt = LJ + (min(jj, jlast) * KC + kk) * 256;
+            if (jj <= jdo) {  // wave-uniform
+              const double* Bt = LJ + (min(jj, jlast) * KC + kk) * 256;
 #pragma unroll
-            for (int r = 0; r < 4; ++r)
-              acc[jj] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[r], Bt[64 * r + lane], acc[jj], 0, 0, MFMA_NEG_A);
+              for (int r = 0; r < 4; ++r)
+                acc[jj] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[r], Bt[64 * r + lane], acc[jj], 0, 0, MFMA_NEG_A);
+            }
           }
         }
       }
