@@ -836,8 +836,9 @@ constexpr int BIG_WIDE_NT = MHE_BIG_WIDE_NT;
 #define MHE_BIG_LLR8 2  // rows per wave of the left-looking update, 8-wide slab instance
 #endif
 #ifndef MHE_BIG_SPLIT
-#define MHE_BIG_SPLIT 2  // the left-looking factorization as per-block-column launches (k_big_chol SPLIT,
-                         // k_big_rows): 2 = for wide systems (NT >= BIG_WIDE_NT: C4, C5), 1 = always, 0 = never
+#define MHE_BIG_SPLIT 1  // the left-looking factorization as per-block-column launches (k_big_chol SPLIT,
+                         // k_big_rows): 1 = always (round 6: C3 too), 2 = for wide systems only (NT >=
+                         // BIG_WIDE_NT: C4, C5; the round-5 default), 0 = never
 #endif
 #ifndef MHE_BIG_TWO_STREAMS
 #define MHE_BIG_TWO_STREAMS 0  // split factorization: the batch's two halves on two streams (C3 +1.4 %, C4 +0.8 %, C5 0 vs one stream)
@@ -848,11 +849,17 @@ constexpr int BIG_WIDE_NT = MHE_BIG_WIDE_NT;
 #ifndef MHE_BIG_DIAG_SKIP
 #define MHE_BIG_DIAG_SKIP 1  // split diagonal stage: skip the MFMAs of tiles past a row's diagonal, SIMD-balanced rows
 #endif
+#ifndef MHE_BIG_DIAG_LROW
+#define MHE_BIG_DIAG_LROW 1  // split diagonal stage: the rows' own L_Ik from the staged slab (LDS), not HBM
+#endif
 #ifndef MHE_BIG_ROWS_KC
-#define MHE_BIG_ROWS_KC 4  // k_big_rows: k tiles per staged slab
+#define MHE_BIG_ROWS_KC 2  // k_big_rows: k tiles per staged slab
 #endif
 #ifndef MHE_BIG_ROWS_DB
-#define MHE_BIG_ROWS_DB 0  // k_big_rows: slabs double-buffered (the next in flight during this one's MFMAs)
+#define MHE_BIG_ROWS_DB 1  // k_big_rows: slabs double-buffered (the next in flight during this one's MFMAs)
+#endif
+#ifndef MHE_BIG_ROWS_RPF
+#define MHE_BIG_ROWS_RPF 1  // k_big_rows: the row's L_Ik loaded a whole slab chunk ahead
 #endif
 #ifndef MHE_BIG_ROWS_XCD
 #define MHE_BIG_ROWS_XCD 1  // k_big_rows: a trajectory's row groups on one XCD (batch % 8 == 0)
@@ -955,8 +962,13 @@ __device__ __forceinline__ void big_diag_block(const BigArgs& a, int k0, int ken
         __syncthreads();  // the previous slab is consumed
         stage_slab_lds(LJ, H, k0, kb, kc, KC, NT);  // L_Jk, J = k0 + jj, k = kc + kk
         __syncthreads();
+        // the row's own L_Ik are slab tiles too (I is one of the block's rows J): read from
+        // LDS (MHE_BIG_DIAG_LROW) instead of a second time from HBM
+        auto lrow = [&](int kk) {
+          return MHE_BIG_DIAG_LROW ? LJ + (jlast * KC + kk) * 256 : H + (size_t)big_tile_index(Ic, kc + kk, NT) * 256;
+        };
         double an[4];
-        const double* L0 = H + (size_t)big_tile_index(Ic, kc, NT) * 256;
+        const double* L0 = lrow(0);
 #pragma unroll
         for (int r = 0; r < 4; ++r) an[r] = L0[64 * r + lane];
 #pragma unroll
@@ -965,7 +977,7 @@ __device__ __forceinline__ void big_diag_block(const BigArgs& a, int k0, int ken
 #pragma unroll
           for (int r = 0; r < 4; ++r) av[r] = an[r];  // negated by the MFMA
           if (kk + 1 < KC) {
-            const double* Ln = H + (size_t)big_tile_index(Ic, kc + kk + 1, NT) * 256;
+            const double* Ln = lrow(kk + 1);
 #pragma unroll
             for (int r = 0; r < 4; ++r) an[r] = Ln[64 * r + lane];
           }
@@ -1483,6 +1495,54 @@ __device__ __forceinline__ void big_rows_group(double* H, const double* LTg, dou
   }
   constexpr int SLAB = BIG_KB * KC * 256;
   if (k0 > 0 && !(MHE_BIG_KO & 1)) stage_slab_lds(sm, H, k0, kb, 0, KC, NT, false);
+#if MHE_BIG_ROWS_RPF
+  // The row's L_Ik (B operands) a whole chunk ahead: tile kc + kk is loaded into bq[kk]
+  // right after chunk kc - KC's MFMAs have read bq[kk], so its HBM latency is covered by
+  // a chunk of MFMAs (and the slab wait) instead of by one k step.
+  double bq[KC][4];
+  if (k0 > 0 && !(MHE_BIG_KO & 1)) {
+#pragma unroll
+    for (int kk = 0; kk < KC; ++kk) {
+      const double* L0 = H + (size_t)big_tile_index(Ic, kk, NT) * 256;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bq[kk][r] = L0[64 * r + lane];
+    }
+  }
+  for (int kc = 0; kc < k0 && !(MHE_BIG_KO & 1); kc += KC) {
+    const double* LJ = sm + (DB ? ((kc / KC) & 1) * SLAB : 0);
+    if (!DB && kc > 0) {
+      __syncthreads();  // the previous chunk's readers are done
+      stage_slab_lds(sm, H, k0, kb, kc, KC, NT, false);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this chunk's slab (and row tiles) have landed
+    __syncthreads();
+    if (DB && kc + KC < k0) stage_slab_lds(sm + (((kc / KC) + 1) & 1) * SLAB, H, k0, kb, kc + KC, KC, NT, false);
+#pragma unroll
+    for (int kk = 0; kk < KC; ++kk) {
+      double a0[4], a1[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) a0[r] = LJ[kk * 256 + 64 * r + lane];
+#pragma unroll
+      for (int jj = 0; jj < BIG_KB; ++jj) {
+        if (jj + 1 < BIG_KB) {
+          const int jn = min(jj + 1, kb - 1);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) a1[r] = LJ[(jn * KC + kk) * 256 + 64 * r + lane];
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          acc[jj] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0[r], bq[kk][r], acc[jj], 0, 0, MFMA_NEG_A);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) a0[r] = a1[r];
+      }
+      if (kc + KC < k0) {  // the next chunk's tile kk (its MFMAs above have read bq[kk])
+        const double* Ln = H + (size_t)big_tile_index(Ic, kc + KC + kk, NT) * 256;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bq[kk][r] = Ln[64 * r + lane];
+      }
+    }
+  }
+#else
   for (int kc = 0; kc < k0 && !(MHE_BIG_KO & 1); kc += KC) {
     const double* LJ = sm + (DB ? ((kc / KC) & 1) * SLAB : 0);
     if (!DB && kc > 0) {
@@ -1525,6 +1585,7 @@ __device__ __forceinline__ void big_rows_group(double* H, const double* LTg, dou
       }
     }
   }
+#endif
   // the block's in-block L tiles and L_kk^-T into LDS (over the slabs)
   __syncthreads();
   for (int e = threadIdx.x; e < (kb * (kb - 1) / 2) * 128; e += BIG_NTHREADS) {

@@ -46,6 +46,9 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 #ifndef MHE_NW
 #define MHE_NW 8
 #endif
+#ifndef MHE_SB_DIAG_BUILD
+#define MHE_SB_DIAG_BUILD 0  // A/B: small-batch instance's diagonal tiles built by waves 0 and 4 only
+#endif
 constexpr int NW = MHE_NW;
 constexpr int NTHREADS = NW * 64;
 constexpr int MAX_NT = 13;         // padded system <= 208 (register-resident path)
@@ -904,7 +907,7 @@ __device__ __forceinline__ void build_slots_n2(const GnArgs& a, const ConstLayou
 // BOUNDED (projected Newton, k_gn_bounded): rows and columns of the epsilon-active
 // unknowns (ACT) are replaced by their diagonal entries -- the reduced GN system on
 // the free unknowns, a diagonally scaled gradient step on the active ones.
-template <class DYN, class MEAS, int SLOTS, bool HUBER = false, bool BOUNDED = false>
+template <class DYN, class MEAS, int SLOTS, bool HUBER = false, bool BOUNDED = false, bool SB = false>
 __device__ __forceinline__ void build_tiles(const GnArgs& a, const ConstLayout& CL, const SmemLayout& SL, double* sm,
                                             d4 (&acc)[SLOTS], int wave, int lane, int stab) {
   const int* ACT = (const int*)(sm + SL.ACT);
@@ -998,7 +1001,12 @@ __device__ __forceinline__ void build_tiles(const GnArgs& a, const ConstLayout& 
     if (s & 1) __builtin_amdgcn_sched_barrier(0);
   }
   double* DT = sm + SL.DT;
-  for (int J = wave; J < a.NT; J += NW) {
+  // small-batch factorization: the diagonal tiles go to the two waves without slots (CP,
+  // wave 0, and wave 4), alternately, instead of one or two to every wave -- the six
+  // slot owners build only their off-diagonal tiles (MHE_SB_DIAG_BUILD)
+  const bool sbd = SB && MHE_SB_DIAG_BUILD;
+  const int j0 = sbd ? (wave == 0 ? 0 : wave == 4 ? 1 : a.NT) : wave, js = sbd ? 2 : NW;
+  for (int J = j0; J < a.NT; J += js) {
     const int ti = tile_index(J, J, a.NT);
     const size_t off = (size_t)ti * 256 + lane;
     const int col = 16 * J + (lane & 15);
@@ -1965,7 +1973,7 @@ __global__ __launch_bounds__(NTHREADS, MINW) void k_gn(GnArgs a) {
       return;
     }
     if (it >= a.max_iter) break;
-    build_tiles<DYN, MEAS, SLOTS, HUBER>(FA, FCL, FSL, sm, acc, wave, lane, stab);
+    build_tiles<DYN, MEAS, SLOTS, HUBER, false, SB>(FA, FCL, FSL, sm, acc, wave, lane, stab);
     DIAG_MARK(15);
     __syncthreads();
     DIAG_MARK(2);
