@@ -852,6 +852,12 @@ constexpr int BIG_WIDE_NT = MHE_BIG_WIDE_NT;
 #ifndef MHE_BIG_DIAG_LROW
 #define MHE_BIG_DIAG_LROW 1  // split diagonal stage: the rows' own L_Ik from the staged slab (LDS), not HBM
 #endif
+#ifndef MHE_BIG_BWD_PF
+#define MHE_BIG_BWD_PF 2  // split solve launch: tiles of the next column each wave has in flight (5: -1 % at C3)
+#endif
+#ifndef MHE_BIG_ROWS_SKIP
+#define MHE_BIG_ROWS_SKIP 1  // k_big_rows: row-less waves skip the left-looking MFMAs
+#endif
 #ifndef MHE_BIG_ROWS_KC
 #define MHE_BIG_ROWS_KC 2  // k_big_rows: k tiles per staged slab
 #endif
@@ -1381,7 +1387,10 @@ __global__ __launch_bounds__(BIG_NTHREADS, BIG_JB == 8 ? 2 : 4) void k_big_chol(
   // wave loads its first BWD_PF tiles of column k - 1 (and wave 0 its four L_kk^-T
   // entries per lane) during step k; y / delta live in LDS (the slab region, free now)
   // when they fit, the global YV copy is written alongside for k_big_update.
-  constexpr int BWD_PF = BIG_JB == 8 ? 4 : 2;
+  // the split form's solve launch (SPLIT = 2) runs nothing else, so its registers can hold
+  // a whole column's tiles for this wave at C3 (NT = 65: <= 8 per wave) -- every tile of
+  // column k - 1 in flight during step k instead of two (MHE_BIG_BWD_PF)
+  constexpr int BWD_PF = SPLIT == 2 ? MHE_BIG_BWD_PF : (BIG_JB == 8 ? 4 : 2);
   const bool yl = NT * 16 <= big_slab_doubles(BIG_JB);
   double* yb = yl ? LJ : YV;
   if (yl) {
@@ -1417,10 +1426,24 @@ __global__ __launch_bounds__(BIG_NTHREADS, BIG_JB == 8 ? 2 : 4) void k_big_chol(
         for (int r = 0; r < 4; ++r) pv += cur[m][r] * yb[16 * I + bg + 4 * r];
       }
     }
-    for (int I = k + 1 + wave + BIG_NW * BWD_PF; I < NT; I += BIG_NW) {  // past the prefetched tiles (C4, C5)
-      const double* L = H + (size_t)big_tile_index(I, k, NT) * 256;
+    // past the prefetched tiles (C4, C5): four tiles' loads issued together
+    for (int I0 = k + 1 + wave + BIG_NW * BWD_PF; I0 < NT; I0 += 4 * BIG_NW) {
+      double t[4][4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) pv += L[bc * 16 + bg + 4 * r] * yb[16 * I + bg + 4 * r];
+      for (int u = 0; u < 4; ++u) {
+        const int I = min(I0 + BIG_NW * u, NT - 1);
+        const double* L = H + (size_t)big_tile_index(I, k, NT) * 256;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) t[u][r] = L[bc * 16 + bg + 4 * r];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int I = I0 + BIG_NW * u;
+        if (I < NT) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) pv += t[u][r] * yb[16 * I + bg + 4 * r];
+        }
+      }
     }
     pv += __shfl_xor(pv, 16);
     pv += __shfl_xor(pv, 32);
@@ -1517,6 +1540,10 @@ __device__ __forceinline__ void big_rows_group(double* H, const double* LTg, dou
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this chunk's slab (and row tiles) have landed
     __syncthreads();
     if (DB && kc + KC < k0) stage_slab_lds(sm + (((kc / KC) + 1) & 1) * SLAB, H, k0, kb, kc + KC, KC, NT, false);
+    // a wave without a row (I >= NT: the last group of every launch) skips the MFMAs by a
+    // wave-uniform branch around the whole chunk (MHE_BIG_ROWS_SKIP); it still stages and
+    // meets the barriers
+    if (MHE_BIG_ROWS_SKIP && !act) continue;
 #pragma unroll
     for (int kk = 0; kk < KC; ++kk) {
       double a0[4], a1[4];
