@@ -138,3 +138,27 @@ def test_integration_stub_declares_the_full_struct():
     assert m, "INTEGRATION.md has no mhe_dims stub"
     names = _re.findall(r'\("([a-z_A-Z]+)"', m.group(1))
     assert names == [f[0] for f in _lib.MheDims._fields_]
+
+
+def test_kkt_dim_and_kernel_name_queries_without_gpu():
+    """Host-only ABI v6 queries: mhe_kkt_dim = padded dim + n_extra + n_eq, and
+    mhe_solve_kernel_name names the instance the launch would pick (batch vs CUs; no
+    device here, so the CU count falls back to 256) or the large-system sequence."""
+    import numpy as np
+    lib = _lib.load()
+    d = _lib.MheDims()
+    d.N, d.n, d.m, d.p, d.M, d.q, d.dyn_model, d.meas_model, d.T = 100, 2, 1, 2, 101, 0, 5, 1, 10.0
+    assert lib.mhe_kkt_dim(d) == lib.mhe_padded_dim(d) == 208
+    buf = ctypes.create_string_buffer(256)
+    assert lib.mhe_solve_kernel_name(d, 1024, None, buf, 256) == 0 and b"two workgroups per CU" in buf.value
+    assert lib.mhe_solve_kernel_name(d, 128, None, buf, 256) == 0 and b"SB=true" in buf.value
+    assert lib.mhe_solve_kernel_name(d, 128, None, None, 0) == -5  # MHE_ERR_NULL
+    d.N = 500
+    assert lib.mhe_solve_kernel_name(d, 8, None, buf, 256) == 0 and buf.value.startswith(b"large-system path")
+    # a bordered problem: equality rows (host pointer) -> dp + n_eq rows
+    eq = np.array([[0, 1], [2, 3], [4, -1]], dtype=np.int32)
+    d.n_eq = 3
+    d.eq_idx = eq.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
+    assert lib.mhe_kkt_dim(d) == lib.mhe_padded_dim(d) + 3
+    d.struct_size = 8  # a truncated struct is refused
+    assert lib.mhe_kkt_dim(d) == -1
