@@ -853,10 +853,13 @@ constexpr int BIG_WIDE_NT = MHE_BIG_WIDE_NT;
 #define MHE_BIG_DIAG_LROW 1  // split diagonal stage: the rows' own L_Ik from the staged slab (LDS), not HBM
 #endif
 #ifndef MHE_BIG_BWD_PF
-#define MHE_BIG_BWD_PF 2  // split solve launch: tiles of the next column each wave has in flight (5: -1 % at C3)
+#define MHE_BIG_BWD_PF 2  // split solve launch: tiles of the next column each wave has in flight (5: slower at C3)
 #endif
 #ifndef MHE_BIG_ROWS_SKIP
 #define MHE_BIG_ROWS_SKIP 1  // k_big_rows: row-less waves skip the left-looking MFMAs
+#endif
+#ifndef MHE_BIG_BWD_COAL
+#define MHE_BIG_BWD_COAL 1  // backward solve: coalesced tile loads, one DPP row reduction per step (C3 +3.7 %, C4 +2.1 %)
 #endif
 #ifndef MHE_BIG_ROWS_KC
 #define MHE_BIG_ROWS_KC 2  // k_big_rows: k tiles per staged slab
@@ -1406,7 +1409,8 @@ __global__ __launch_bounds__(BIG_NTHREADS, BIG_JB == 8 ? 2 : 4) void k_big_chol(
       if (I < NT) {
         const double* L = H + (size_t)big_tile_index(I, k, NT) * 256;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) dst[m][r] = L[bc * 16 + bg + 4 * r];  // L_Ik[tr][bc], k-major tile
+        for (int r = 0; r < 4; ++r)  // L_Ik[tr][bc], k-major tile; coalesced: element (4r + bg) * 16 + bc
+          dst[m][r] = MHE_BIG_BWD_COAL ? L[64 * r + lane] : L[bc * 16 + bg + 4 * r];
       }
     }
     if (wave == 0) {
@@ -1418,36 +1422,43 @@ __global__ __launch_bounds__(BIG_NTHREADS, BIG_JB == 8 ? 2 : 4) void k_big_chol(
   for (int k = NT - 1; k >= 0 && !(MHE_BIG_KO & 32); --k) {
     if (k > 0) load_col(k - 1, nxt, ltn);  // in flight during this step
     double pv = 0.0;
+    double pq[4] = {0.0, 0.0, 0.0, 0.0};  // MHE_BIG_BWD_COAL: output column 4r + bg, this lane's row bc
 #pragma unroll
     for (int m = 0; m < BWD_PF; ++m) {
       const int I = k + 1 + wave + BIG_NW * m;
       if (I < NT) {
+        if (MHE_BIG_BWD_COAL) {
+          const double dI = yb[16 * I + bc];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) pv += cur[m][r] * yb[16 * I + bg + 4 * r];
-      }
-    }
-    // past the prefetched tiles (C4, C5): four tiles' loads issued together
-    for (int I0 = k + 1 + wave + BIG_NW * BWD_PF; I0 < NT; I0 += 4 * BIG_NW) {
-      double t[4][4];
+          for (int r = 0; r < 4; ++r) pq[r] += cur[m][r] * dI;
+        } else {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int I = min(I0 + BIG_NW * u, NT - 1);
-        const double* L = H + (size_t)big_tile_index(I, k, NT) * 256;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) t[u][r] = L[bc * 16 + bg + 4 * r];
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int I = I0 + BIG_NW * u;
-        if (I < NT) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) pv += t[u][r] * yb[16 * I + bg + 4 * r];
+          for (int r = 0; r < 4; ++r) pv += cur[m][r] * yb[16 * I + bg + 4 * r];
         }
       }
     }
-    pv += __shfl_xor(pv, 16);
-    pv += __shfl_xor(pv, 32);
-    if (lane < 16) PART[wave * 16 + lane] = pv;
+    for (int I = k + 1 + wave + BIG_NW * BWD_PF; I < NT; I += BIG_NW) {  // past the prefetched tiles (C4, C5)
+      // (issuing these loads four at a time measured slower: the solve launch 1.23 -> 1.45 ms at C3)
+      const double* L = H + (size_t)big_tile_index(I, k, NT) * 256;
+      if (MHE_BIG_BWD_COAL) {
+        const double dI = yb[16 * I + bc];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pq[r] += L[64 * r + lane] * dI;
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pv += L[bc * 16 + bg + 4 * r] * yb[16 * I + bg + 4 * r];
+      }
+    }
+    if (MHE_BIG_BWD_COAL) {
+      // the 16 rows of each output column are the 16 lanes of a DPP row: lane (bc, bg) ends
+      // with column 4 r(bc) + bg, r(bc) = 2 (bc >> 3) + ((bc >> 2) & 1)
+      const double z = row16_sum4(pq, bc);
+      if ((bc & 3) == 0) PART[wave * 16 + 4 * (2 * (bc >> 3) + ((bc >> 2) & 1)) + bg] = z;
+    } else {
+      pv += __shfl_xor(pv, 16);
+      pv += __shfl_xor(pv, 32);
+      if (lane < 16) PART[wave * 16 + lane] = pv;
+    }
     __syncthreads();
     if (wave == 0) {
       if (lane < 16) {
