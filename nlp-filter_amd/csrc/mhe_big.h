@@ -861,6 +861,9 @@ constexpr int BIG_WIDE_NT = MHE_BIG_WIDE_NT;
 #ifndef MHE_BIG_BWD_COAL
 #define MHE_BIG_BWD_COAL 1  // backward solve: coalesced tile loads, one DPP row reduction per step (C3 +3.7 %, C4 +2.1 %)
 #endif
+#ifndef MHE_BIG_ROWS_TLDS
+#define MHE_BIG_ROWS_TLDS 1  // k_big_rows: the row's A_Ik^T read coalesced and transposed through LDS (C3 +1.8 %, C4 +1.1 %)
+#endif
 #ifndef MHE_BIG_ROWS_KC
 #define MHE_BIG_ROWS_KC 2  // k_big_rows: k tiles per staged slab
 #endif
@@ -1521,13 +1524,36 @@ __device__ __forceinline__ void big_rows_group(double* H, const double* LTg, dou
   const bool act = I < NT;
   const int Ic = act ? I : NT - 1;
   d4 acc[BIG_KB];
-#pragma unroll
-  for (int kk = 0; kk < BIG_KB; ++kk) {
-    const double* A = H + (size_t)big_tile_index(Ic, k0 + min(kk, kb - 1), NT) * 256;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) acc[kk][r] = A[c * 16 + 4 * r + g];  // A_Ik^T, k-major
-  }
   constexpr int SLAB = BIG_KB * KC * 256;
+  if constexpr (MHE_BIG_ROWS_TLDS && DB) {
+    // A_Ik^T through LDS: the tiles read coalesced (element 64 r + lane = A[4r + g][c]), then
+    // transposed through this wave's padded 16 x 17 scratch in the second slab buffer (first
+    // staged at chunk 1, after a barrier) -- the per-lane transposed global reads touched 16
+    // cache lines per instruction
+#pragma unroll
+    for (int kk = 0; kk < BIG_KB; ++kk) {
+      const double* A = H + (size_t)big_tile_index(Ic, k0 + min(kk, kb - 1), NT) * 256;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[kk][r] = A[64 * r + lane];
+    }
+    double* T = sm + SLAB + wave * 272;
+#pragma unroll
+    for (int kk = 0; kk < BIG_KB; ++kk) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) T[(4 * r + g) * 17 + c] = acc[kk][r];
+      wave_lds_sync();
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[kk][r] = T[c * 17 + g + 4 * r];  // A_Ik^T, k-major
+      wave_lds_sync();
+    }
+  } else {
+#pragma unroll
+    for (int kk = 0; kk < BIG_KB; ++kk) {
+      const double* A = H + (size_t)big_tile_index(Ic, k0 + min(kk, kb - 1), NT) * 256;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[kk][r] = A[c * 16 + 4 * r + g];  // A_Ik^T, k-major
+    }
+  }
   if (k0 > 0 && !(MHE_BIG_KO & 1)) stage_slab_lds(sm, H, k0, kb, 0, KC, NT, false);
 #if MHE_BIG_ROWS_RPF
   // The row's L_Ik (B operands) a whole chunk ahead: tile kc + kk is loaded into bq[kk]
