@@ -26,6 +26,9 @@
 // Converged or failed trajectories are frozen by a per-trajectory state word,
 // so the host loop only enqueues (no synchronisation).
 
+#ifndef MHE_BIG_RESID_LDS
+#define MHE_BIG_RESID_LDS 1  // k_big_resid: X staged in LDS for the node / epoch dot products (C3 +0.7 %)
+#endif
 constexpr int BIG_NW = 8;
 constexpr int BIG_NTHREADS = BIG_NW * 64;
 constexpr int BIG_RUNNING = -1;
@@ -295,7 +298,15 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_resid(BigArgs a, int final
   const int* erow = (const int*)(a.cbuf + CL.erow);
   const int E = a.M > 0 ? *(const int*)(a.cbuf + CL.ne) : 0;
   const int Mr = a.M > 0 ? a.M : 1;
-  const double* X = a.X + (size_t)b * a.P * n;
+  // X staged in LDS (MHE_BIG_RESID_LDS; dynamic LDS of P n doubles): every thread's node
+  // and epoch dot products read all of X, as LDS broadcasts instead of L1/L2 loads
+  extern __shared__ __attribute__((aligned(16))) double xl_dyn[];
+  const double* Xg = a.X + (size_t)b * a.P * n;
+  if (MHE_BIG_RESID_LDS) {
+    for (int t = threadIdx.x; t < a.P * n; t += BIG_NTHREADS) xl_dyn[t] = Xg[t];
+    __syncthreads();
+  }
+  const double* X = MHE_BIG_RESID_LDS ? xl_dyn : Xg;
   __shared__ double red[2 * BIG_NW];
   double cost = 0.0, noise = 0.0;  // noise: the cost's rounding level (bounded problems' line search)
   // interpolated states at the epochs: x_e = sum_j Phi_E[e][j] X_j

@@ -2650,6 +2650,17 @@ inline BigAsmShape big_asm_shape(const BigArgs& A) {
   return s;
 }
 
+// k_big_resid with its dynamic LDS (X staged when MHE_BIG_RESID_LDS: P n doubles; C5 64 KB)
+template <class DYN, class MEAS>
+inline int launch_big_resid(const BigArgs& A, int batch, int final_pass, hipStream_t st) {
+  const int smem = MHE_BIG_RESID_LDS ? A.P * A.n * (int)sizeof(double) : 0;
+  if (smem > 0 && hipFuncSetAttribute((const void*)k_big_resid<DYN, MEAS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      smem) != hipSuccess)
+    return MHE_ERR_HIP;
+  hipLaunchKernelGGL((k_big_resid<DYN, MEAS>), dim3(batch), dim3(BIG_NTHREADS), smem, st, A, final_pass);
+  return MHE_OK;
+}
+
 // Kernel-level parity stages of the large-system path (mhe_assemble_ws /
 // mhe_chol_solve_ws): BIG_STAGE_ASSEMBLE runs k_big_resid + k_big_assemble at A.X (H
 // tiles and BV = -g in the workspace, cost; with z also the per-epoch border sums),
@@ -2663,7 +2674,7 @@ int launch_big_stage(const mhe_dims* dm, BigArgs& A, int batch, int stage, hipSt
   if (stage == BIG_STAGE_ASSEMBLE) {
     big_pair_plan(A, BigGSupport<MEAS>::get(A.idx, A.n));
     const BigAsmShape sh = big_asm_shape(A);
-    hipLaunchKernelGGL((k_big_resid<DYN, MEAS>), dim3(batch), dim3(BIG_NTHREADS), 0, st, A, 0);
+    if (launch_big_resid<DYN, MEAS>(A, batch, 0, st) != MHE_OK) return MHE_ERR_HIP;
     hipLaunchKernelGGL((k_big_assemble<DYN, MEAS>), dim3(sh.blocks, batch), dim3(64 * sh.wpb), sh.lds, st, A);
   } else {
     BigCholPlan cp;
@@ -2703,7 +2714,7 @@ int launch_big(const mhe_dims* dm, BigArgs& A, int batch, int max_iter, hipStrea
   }
   const BigAsmShape sh = big_asm_shape(A);
   for (int it = 0; it < max_iter; ++it) {
-    hipLaunchKernelGGL((k_big_resid<DYN, MEAS>), dim3(batch), dim3(BIG_NTHREADS), 0, st, A, 0);
+    if (launch_big_resid<DYN, MEAS>(A, batch, 0, st) != MHE_OK) return MHE_ERR_HIP;
     hipLaunchKernelGGL((k_big_assemble<DYN, MEAS>), dim3(sh.blocks, batch), dim3(64 * sh.wpb), sh.lds, st, A);
     launch_big_factor(cp, A, batch, st);
     if (K > 0) hipLaunchKernelGGL((k_big_border<DYN::n, MEAS::p>), dim3(batch), dim3(BIG_NTHREADS), smem_b, st, A);
@@ -2712,7 +2723,7 @@ int launch_big(const mhe_dims* dm, BigArgs& A, int batch, int max_iter, hipStrea
     else
       hipLaunchKernelGGL((k_big_update<DYN::n>), dim3(batch), dim3(256), 0, st, A);
   }
-  hipLaunchKernelGGL((k_big_resid<DYN, MEAS>), dim3(batch), dim3(BIG_NTHREADS), 0, st, A, 1);
+  if (launch_big_resid<DYN, MEAS>(A, batch, 1, st) != MHE_OK) return MHE_ERR_HIP;
   return hipGetLastError() == hipSuccess ? MHE_OK : MHE_ERR_HIP;
 }
 
