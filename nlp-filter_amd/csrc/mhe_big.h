@@ -875,6 +875,9 @@ constexpr int BIG_WIDE_NT = MHE_BIG_WIDE_NT;
 #ifndef MHE_BIG_ROWS_TLDS
 #define MHE_BIG_ROWS_TLDS 1  // k_big_rows: the row's A_Ik^T read coalesced and transposed through LDS (C3 +1.8 %, C4 +1.1 %)
 #endif
+#ifndef MHE_BIG_ROWS_LBDMA
+#define MHE_BIG_ROWS_LBDMA 1  // k_big_rows: the in-block L tiles and L_kk^-T staged by LDS-DMA (C3 +2.4 %, C4 0)
+#endif
 #ifndef MHE_BIG_ROWS_KC
 #define MHE_BIG_ROWS_KC 2  // k_big_rows: k tiles per staged slab
 #endif
@@ -1663,15 +1666,37 @@ __device__ __forceinline__ void big_rows_group(double* H, const double* LTg, dou
 #endif
   // the block's in-block L tiles and L_kk^-T into LDS (over the slabs)
   __syncthreads();
-  for (int e = threadIdx.x; e < (kb * (kb - 1) / 2) * 128; e += BIG_NTHREADS) {
-    const int slot = e >> 7;
-    int ii = 1;  // slot = ii (ii - 1) / 2 + kp, kp < ii
-    while (ii * (ii + 1) / 2 <= slot) ++ii;
-    const int kp = slot - ii * (ii - 1) / 2;
-    const double2 w = *(const double2*)(H + (size_t)big_tile_index(k0 + ii, k0 + kp, NT) * 256 + 2 * (e & 127));
-    *(double2*)(LB + 256 * slot + 2 * (e & 127)) = w;
+  if constexpr (MHE_BIG_ROWS_LBDMA) {
+    // by LDS-DMA, every wave's share issued at once and waited for once (the load -> store
+    // loop made one L2 round trip per 8 KB: ~19 of them before the in-block chain could start)
+    const int nlb = kb * (kb - 1) / 2 * 2;  // half tiles (1 KB: one wave instruction each)
+    for (int h = wave; h < nlb; h += BIG_NW) {
+      const int slot = h >> 1;
+      int ii = 1;  // slot = ii (ii - 1) / 2 + kp, kp < ii
+      while (ii * (ii + 1) / 2 <= slot) ++ii;
+      const int kp = slot - ii * (ii - 1) / 2;
+      const double* src = H + (size_t)big_tile_index(k0 + ii, k0 + kp, NT) * 256 + 128 * (h & 1) + 2 * lane;
+      __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(LB + 256 * slot + 128 * (h & 1)),
+                                       16, 0, 0);
+    }
+    const int nlt = (kb * DTS) / 2;  // 16-B chunks of the block's L_kk^-T (kb * DTS is even)
+    for (int c0 = wave * 64; c0 < nlt; c0 += BIG_NTHREADS) {
+      if (c0 + lane < nlt)
+        __builtin_amdgcn_global_load_lds((const void*)(LTg + (size_t)k0 * DTS + 2 * (c0 + lane)),
+                                         (__attribute__((address_space(3))) void*)(LTs + 2 * c0), 16, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    for (int e = threadIdx.x; e < (kb * (kb - 1) / 2) * 128; e += BIG_NTHREADS) {
+      const int slot = e >> 7;
+      int ii = 1;  // slot = ii (ii - 1) / 2 + kp, kp < ii
+      while (ii * (ii + 1) / 2 <= slot) ++ii;
+      const int kp = slot - ii * (ii - 1) / 2;
+      const double2 w = *(const double2*)(H + (size_t)big_tile_index(k0 + ii, k0 + kp, NT) * 256 + 2 * (e & 127));
+      *(double2*)(LB + 256 * slot + 2 * (e & 127)) = w;
+    }
+    for (int e = threadIdx.x; e < kb * DTS; e += BIG_NTHREADS) LTs[e] = LTg[(size_t)k0 * DTS + e];
   }
-  for (int e = threadIdx.x; e < kb * DTS; e += BIG_NTHREADS) LTs[e] = LTg[(size_t)k0 * DTS + e];
   __syncthreads();
 #pragma unroll
   for (int kk = 0; kk < BIG_KB; ++kk) {
