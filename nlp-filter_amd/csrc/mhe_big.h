@@ -26,6 +26,9 @@
 // Converged or failed trajectories are frozen by a per-trajectory state word,
 // so the host loop only enqueues (no synchronisation).
 
+#ifndef MHE_BIG_DIAG_DB
+#define MHE_BIG_DIAG_DB 1  // split diagonal stage: KC = 2 double-buffered slabs (C3 +0.8 %, C4 0)
+#endif
 #ifndef MHE_BIG_RESID_LDS
 #define MHE_BIG_RESID_LDS 1  // k_big_resid: X staged in LDS for the node / epoch dot products (C3 +0.7 %)
 #endif
@@ -964,7 +967,12 @@ __device__ __forceinline__ void big_diag_block(const BigArgs& a, int k0, int ken
     // orientation (the diagonal block below reads them from H).  Branch-free: tiles past
     // the row's diagonal and waves without a row compute on clamped tiles, stores only.
     // Same operations and order per element as the pass below.
-    constexpr int KC = 4;
+    // MHE_BIG_DIAG_DB: KC = 2 slabs double-buffered (the next chunk's LDS-DMA in flight
+    // during this one's MFMAs; 2 x 32 KB in the LJ region), else KC = 4 single-buffered
+    constexpr bool DDB = MHE_BIG_DIAG_DB != 0;
+    constexpr int KC = DDB ? 2 : 4;
+    constexpr int SLABD = BIG_KB * KC * 256;
+    static_assert(!DDB || 2 * SLABD <= BIG_LB_TILES * 256 + BIG_KB * DTS, "both slabs fit the LJ region");
     const int kb = kend - k0;
     if (k0 > 0 && !(MHE_BIG_KO & 1)) {
       const int wv = __builtin_amdgcn_readfirstlane(wave);
@@ -984,14 +992,22 @@ __device__ __forceinline__ void big_diag_block(const BigArgs& a, int k0, int ken
 #pragma unroll
         for (int r = 0; r < 4; ++r) acc[jj][r] = C[64 * r + lane];
       }
+      if (DDB) stage_slab_lds(LJ, H, k0, kb, 0, KC, NT, false);
       for (int kc = 0; kc < k0; kc += KC) {
-        __syncthreads();  // the previous slab is consumed
-        stage_slab_lds(LJ, H, k0, kb, kc, KC, NT);  // L_Jk, J = k0 + jj, k = kc + kk
-        __syncthreads();
+        double* S = LJ + (DDB ? ((kc / KC) & 1) * SLABD : 0);
+        if (DDB) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this chunk's slab has landed
+          __syncthreads();  // ... for every wave; the other buffer's readers are done
+          if (kc + KC < k0) stage_slab_lds(LJ + (((kc / KC) + 1) & 1) * SLABD, H, k0, kb, kc + KC, KC, NT, false);
+        } else {
+          __syncthreads();  // the previous slab is consumed
+          stage_slab_lds(LJ, H, k0, kb, kc, KC, NT);  // L_Jk, J = k0 + jj, k = kc + kk
+          __syncthreads();
+        }
         // the row's own L_Ik are slab tiles too (I is one of the block's rows J): read from
         // LDS (MHE_BIG_DIAG_LROW) instead of a second time from HBM
         auto lrow = [&](int kk) {
-          return MHE_BIG_DIAG_LROW ? LJ + (jlast * KC + kk) * 256 : H + (size_t)big_tile_index(Ic, kc + kk, NT) * 256;
+          return MHE_BIG_DIAG_LROW ? S + (jlast * KC + kk) * 256 : H + (size_t)big_tile_index(Ic, kc + kk, NT) * 256;
         };
         double an[4];
         const double* L0 = lrow(0);
@@ -1010,7 +1026,7 @@ __device__ __forceinline__ void big_diag_block(const BigArgs& a, int k0, int ken
 #pragma unroll
           for (int jj = 0; jj < BIG_KB; ++jj) {
             if (jj <= jdo) {  // wave-uniform
-              const double* Bt = LJ + (min(jj, jlast) * KC + kk) * 256;
+              const double* Bt = S + (min(jj, jlast) * KC + kk) * 256;
 #pragma unroll
               for (int r = 0; r < 4; ++r)
                 acc[jj] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[r], Bt[64 * r + lane], acc[jj], 0, 0, MFMA_NEG_A);
