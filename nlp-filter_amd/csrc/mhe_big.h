@@ -902,7 +902,21 @@ constexpr int BIG_WIDE_NT = MHE_BIG_WIDE_NT;
                       // 16 the rows below the diagonal block, 32 the backward solve; any
                       // nonzero mask also freezes X (k_big_update), 64 only that (the baseline)
 #endif
+#ifndef MHE_BIG_HEAD
+#define MHE_BIG_HEAD 1  // split form: the NT % 8 leftover tile columns as the FIRST block column, so every
+                        // rows launch has whole groups of 8 rows (C3: NT = 65; +9.8 %)
+#endif
 constexpr int BIG_LB_TILES = BIG_KB * (BIG_KB - 1) / 2;
+// End of the split form's block column that starts at k0.  Block columns are 8 wide; with
+// MHE_BIG_HEAD the NT % 8 leftover columns form the first one instead of the last, so the
+// rows below every block column are a multiple of 8 (k_big_rows: one workgroup per 8 rows;
+// at C3, NT = 65, a trailing 1-wide block left one row in the last group of EVERY rows
+// launch).  Tile results do not depend on the partition: each tile's updates accumulate
+// in ascending k in every form.
+__host__ __device__ inline int big_split_kend(int k0, int NT) {
+  const int h = MHE_BIG_HEAD ? NT % BIG_KB : 0;
+  return (k0 == 0 && h != 0) ? h : (k0 + BIG_KB < NT ? k0 + BIG_KB : NT);
+}
 // the LJ region: the trailing slab, or (panel phase) the in-block L tiles LB and the
 // block's L_kk^-T matrices LTs
 __host__ __device__ constexpr int big_slab_doubles(int JB) {
@@ -976,6 +990,7 @@ __device__ __forceinline__ void big_diag_block(const BigArgs& a, int k0, int ken
     constexpr int KC = DDB ? 2 : 4;
     constexpr int SLABD = BIG_KB * KC * 256;
     static_assert(!DDB || 2 * SLABD <= BIG_LB_TILES * 256 + BIG_KB * DTS, "both slabs fit the LJ region");
+    static_assert(!MHE_BIG_HEAD || KC <= 2, "k0 need not be a multiple of KC: a chunk's tiles must stay below the diagonal");
     const int kb = kend - k0;
     if (k0 > 0 && !(MHE_BIG_KO & 1)) {
       const int wv = __builtin_amdgcn_readfirstlane(wave);
@@ -1018,6 +1033,7 @@ __device__ __forceinline__ void big_diag_block(const BigArgs& a, int k0, int ken
         for (int r = 0; r < 4; ++r) an[r] = L0[64 * r + lane];
 #pragma unroll
         for (int kk = 0; kk < KC; ++kk) {
+          if (MHE_BIG_HEAD && kc + kk >= k0) break;  // k0 odd (MHE_BIG_HEAD): the chunk's last tile is past it
           double av[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) av[r] = an[r];  // negated by the MFMA
@@ -1275,9 +1291,9 @@ __global__ __launch_bounds__(BIG_NTHREADS, BIG_JB == 8 ? 2 : 4) void k_big_chol(
   const int NT = a.NT;
   if (threadIdx.x == 0) *flag = 0;
   init_units(UN);
-  const int kbeg = SPLIT == 1 ? kfirst : 0, kstop = SPLIT == 1 ? min(kfirst + BIG_KB, NT) : (SPLIT == 2 ? 0 : NT);
+  const int kbeg = SPLIT == 1 ? kfirst : 0, kstop = SPLIT == 1 ? big_split_kend(kfirst, NT) : (SPLIT == 2 ? 0 : NT);
   for (int k0 = kbeg; k0 < kstop; k0 += BIG_KB) {
-    const int kend = min(k0 + BIG_KB, NT);
+    const int kend = SPLIT == 1 ? kstop : min(k0 + BIG_KB, NT);
     big_diag_block<BIG_JB, LL, SPLIT != 0>(a, k0, kend, H, LTg, BV, YV, sm, lane, wave);
     double* LB = LJ;  // the diagonal block's L_Ik' and L_kk^-T (big_diag_block)
     double* LTs = LJ + BIG_LB_TILES * 256;
@@ -1562,9 +1578,10 @@ template <int KC, bool DB>
 __device__ __forceinline__ void big_rows_group(double* H, const double* LTg, double* BV, const double* YV,
                                                double* sm, int NT, int k0, int grp) {
   static_assert((DB ? 2 : 1) * BIG_KB * KC * 256 <= big_rows_lds(), "the slabs fit the LDS region");
+  static_assert(!MHE_BIG_HEAD || KC <= 2, "k0 need not be a multiple of KC: a chunk's tiles must stay below the diagonal");
   double* LB = sm;
   double* LTs = sm + BIG_LB_TILES * 256;
-  const int kend = min(k0 + BIG_KB, NT), kb = kend - k0;
+  const int kend = big_split_kend(k0, NT), kb = kend - k0;
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = lane >> 4, c = lane & 15;
   // Branch-free over the accumulators (a conditionally updated accumulator costs phi copies
@@ -1633,6 +1650,7 @@ __device__ __forceinline__ void big_rows_group(double* H, const double* LTg, dou
     if (MHE_BIG_ROWS_SKIP && !act) continue;
 #pragma unroll
     for (int kk = 0; kk < KC; ++kk) {
+      if (MHE_BIG_HEAD && kc + kk >= k0) break;  // k0 odd (MHE_BIG_HEAD): no next chunk either
       double a0[4], a1[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) a0[r] = LJ[kk * 256 + 64 * r + lane];
@@ -1672,6 +1690,7 @@ __device__ __forceinline__ void big_rows_group(double* H, const double* LTg, dou
     for (int r = 0; r < 4; ++r) bn[r] = L0[64 * r + lane];
 #pragma unroll
     for (int kk = 0; kk < KC; ++kk) {
+      if (MHE_BIG_HEAD && kc + kk >= k0) break;
       double bv[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) bv[r] = bn[r];
@@ -1736,6 +1755,7 @@ __device__ __forceinline__ void big_rows_group(double* H, const double* LTg, dou
   __syncthreads();
 #pragma unroll
   for (int kk = 0; kk < BIG_KB; ++kk) {
+    if (MHE_BIG_HEAD && kk >= kb) break;  // a narrow (head) block: no work past its columns
     d4 cc = acc[kk];
 #pragma unroll
     for (int kp = 0; kp < kk; ++kp) {

@@ -2569,10 +2569,11 @@ inline void launch_big_split(const BigCholPlan& p, BigArgs A, int boff, int nb, 
                              hipEvent_t after_first = nullptr) {
   A.ws += (size_t)boff * A.ws_stride;  // the stages index trajectories by workgroup only
   A.state += boff;
-  for (int k0 = 0; k0 < A.NT; k0 += BIG_KB) {
+  for (int k0 = 0, kend; k0 < A.NT; k0 = kend) {
     hipLaunchKernelGGL(p.diag, dim3(nb), dim3(BIG_NTHREADS), p.smem_diag, st, A, k0);
     if (k0 == 0 && after_first) (void)hipEventRecord(after_first, st);
-    const int kend = k0 + BIG_KB < A.NT ? k0 + BIG_KB : A.NT;
+    kend = big_split_kend(k0, A.NT);  // the same partition as the stages'
+
     if (kend < A.NT)
       hipLaunchKernelGGL(k_big_rows<>, dim3((A.NT - kend + BIG_NW - 1) / BIG_NW, nb), dim3(BIG_NTHREADS),
                          p.smem_rows, st, A, k0);
