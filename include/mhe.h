@@ -111,7 +111,7 @@ extern "C" {
  * the size queries) unless it equals this build's sizeof -- a binding that
  * declares an older or truncated struct is refused before any later field is
  * read.  (mhe/_lib.py sets it in the ctypes constructors.) */
-#define MHE_ABI_VERSION 6
+#define MHE_ABI_VERSION 7
 
 typedef struct mhe_dims {
   int32_t struct_size;  /* = sizeof(mhe_dims)                                */
@@ -411,6 +411,19 @@ int32_t mhe_kkt_dim(const mhe_dims* dims);
  * or the large-system path's kernel sequence.  Host-only query; launches nothing.
  * (bench.py names the roofline record's kernel with it.) */
 int32_t mhe_solve_kernel_name(const mhe_dims* dims, int32_t batch, void* stream, char* buf, int32_t len);
+
+/* The envelope the large-system path's split factorization used (ABI v7): for
+ * trajectory `traj` of the last solve / mhe_chol_solve_ws run on `workspace`
+ * (workspace_bytes as passed there), the first nonzero tile column of each of its
+ * NT = dp / 16 component-major tile rows (the factor has no nonzero tile left of it;
+ * the left-looking updates and the backward solve skip those tiles), NT int32 into
+ * first_col (n_out >= NT).  Formed on the device from the component pairs whose block
+ * of H has a nonzero element at the iterate.  Synchronises `stream` (a copy to the
+ * host); returns NT, MHE_ERR_UNSUPPORTED on the register path or in a build without
+ * the envelope (every column then starts at 0), MHE_ERR_NULL / MHE_ERR_DIMS on bad
+ * arguments.  Used by tools/bench_big.py for the executed flop count. */
+int32_t mhe_big_envelope(const mhe_dims* dims, const void* workspace, size_t workspace_bytes, int32_t traj,
+                         int32_t* first_col, int32_t n_out, void* stream);
 int mhe_assemble_kkt_ws(const mhe_dims* dims, const void* const_buf, int32_t batch,
                         const double* X, const double* Z, const double* U, int64_t u_bstride,
                         const double* Y, const double* PAR, int64_t par_bstride,

@@ -29,6 +29,9 @@
 #ifndef MHE_BIG_DIAG_DB
 #define MHE_BIG_DIAG_DB 1  // split diagonal stage: KC = 2 double-buffered slabs (C3 +0.8 %, C4 0)
 #endif
+#ifndef MHE_BIG_ENV
+#define MHE_BIG_ENV 1  // split form: skip the tiles outside the factor's envelope (component-pair sparsity; C5 5.8x, C3 +8 %)
+#endif
 #ifndef MHE_BIG_DIAG_AKPF
 #define MHE_BIG_DIAG_AKPF 1  // diagonal block: the next diagonal tile loaded one column ahead (+0.3 %)
 #endif
@@ -68,7 +71,7 @@ __host__ __device__ inline BigConst big_const_layout(int P, int M, int n, int p,
 }
 
 struct BigWs {  // per-trajectory workspace offsets in doubles
-  size_t H, LT, BV, YV, XE, GEe, Ge, Es, FtE, Vs, FtV, GZe, HZZe, GZVe, BM, ZM, DZ, ACT, GV, NZ, LAM, KS, total;
+  size_t H, LT, BV, YV, XE, GEe, Ge, Es, FtE, Vs, FtV, GZe, HZZe, GZVe, BM, ZM, DZ, ACT, GV, NZ, LAM, KS, ENV, total;
 };
 
 // nz extra variables, nc equality constraints (border of the KKT system)
@@ -104,9 +107,24 @@ __host__ __device__ inline BigWs big_ws_layout(int P, int M, int n, int NT, int 
   W.LAM = o;  o = al(o + (size_t)P * n);                         // Huber IRLS weights c_k lambda_ka
   W.KS = o;   o = al(o + (size_t)K * K + 2 * K);                 // border: S (K x K), r, w of the last
                                                                  // bordered step (kernel-level KKT parity)
+  W.ENV = o;  o = al(o + ((size_t)n * n + NT + 1) / 2);          // envelope (ints): n x n component-pair
+                                                                 // nonzero flags, then each tile row's
+                                                                 // first nonzero tile column (big_env_*)
   W.total = o;
   return W;
 }
+// The envelope of the split factorization.  k_big_assemble (or the kernel-level import)
+// flags every component pair (a, b) whose block of H has a nonzero element; tile row I of
+// component a then has no nonzero tile left of f(I) = NTc * min{b : (a, b) flagged}, and
+// neither has the Cholesky factor (fill stays inside the envelope of A's rows), so the
+// left-looking updates start at the rows' f, and the backward solve skips the tiles left
+// of them.  Skipped terms are products with exact zeros: the iterates are those of the
+// dense forms (C5's eight receivers: a receiver's components couple to its own and, by
+// the range rows, to the previous receiver's positions -- 1/17 of the dense work).
+__device__ __forceinline__ int* big_env_mask(const double* ws, const BigWs& WL) {
+  return (int*)const_cast<double*>(ws + WL.ENV);
+}
+__device__ __forceinline__ int* big_env_first(const double* ws, const BigWs& WL, int n) { return big_env_mask(ws, WL) + n * n; }
 
 constexpr int BIG_MAX_PAIRS = 44 * 45 / 2;  // component pairs (ca >= cb) of the largest model (n = 40 + z)
 
@@ -293,6 +311,10 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_resid(BigArgs a, int final
   const BigConst CL = big_const_layout(a.P, a.M, n, p, a.nc);
   const BigWs WL = big_ws_layout(a.P, a.M, n, a.NT, a.nz, a.nc);
   double* ws = a.ws + (size_t)b * a.ws_stride;
+  if (MHE_BIG_ENV) {  // the component-pair flags k_big_assemble sets at this iterate
+    int* EM = big_env_mask(ws, WL);
+    for (int t = threadIdx.x; t < n * n; t += BIG_NTHREADS) EM[t] = 0;
+  }
   const double* D = (const double*)(a.cbuf + CL.D);
   const double* Dt = (const double*)(a.cbuf + CL.Dt);
   const double* cw = (const double*)(a.cbuf + CL.cw);
@@ -782,6 +804,7 @@ __global__ __launch_bounds__(256, 4) void k_big_assemble(BigArgs a) {
       // E_l[ca][cb] and E_j[cb][ca] (component-major: node index fastest)
       const int sE1 = (int)((WL.Es + (size_t)(ca * n + cb) * P) * 8), sE2 = (int)((WL.Es + (size_t)(cb * n + ca) * P) * 8);
       const int sF = (int)(WL.FtE * 8) + (ca * n + cb) * 8;
+      bool nzv = false;  // any nonzero element in the tile (MHE_BIG_ENV)
       // tile (it, jt) of block (ca, cb) and, off the diagonal pair, its transpose into (jt, it)
 #pragma unroll
       for (int tp = 0; tp < 2; ++tp) {
@@ -814,8 +837,14 @@ __global__ __launch_bounds__(256, 4) void k_big_assemble(BigArgs a) {
             const int gr = 16 * I + tr, gc = 16 * J + tc;
             if ((ACT[gr] | ACT[gc]) && gr != gc) v = 0.0;
           }
+          if (MHE_BIG_ENV && tp == 0) nzv |= v != 0.0;
           __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(mhe_u2, v), rh, (tr * 16 + tc) * 8, sT, 0);
         }
+      }
+      if (MHE_BIG_ENV && __builtin_amdgcn_ballot_w64(nzv) != 0 && lane == 0) {
+        int* EM = big_env_mask(ws, WL);  // k_big_resid cleared the flags (plain stores: every writer stores 1)
+        EM[ca * n + cb] = 1;
+        EM[cb * n + ca] = 1;
       }
     }
   }
@@ -971,7 +1000,7 @@ __device__ __forceinline__ void stage_slab_lds(double* LJ, const double* H, int 
 // YV, b_I updated).  LDS as k_big_chol's (DT, flag, UN, LJ); a non-SPD pivot sets *flag.
 template <int BIG_JB, bool LL, bool SPLITROWS>
 __device__ __forceinline__ void big_diag_block(const BigArgs& a, int k0, int kend, double* H, double* LTg, double* BV,
-                                               double* YV, double* sm, int lane, int wave) {
+                                               double* YV, double* sm, int lane, int wave, const int* FI = nullptr) {
   double* DT = sm;
   int* flag = (int*)(sm + DTS + BIG_NW * 16 + 16);
   double* UN = sm + DTS + BIG_NW * 16 + 16 + 2;
@@ -1010,13 +1039,22 @@ __device__ __forceinline__ void big_diag_block(const BigArgs& a, int k0, int ken
 #pragma unroll
         for (int r = 0; r < 4; ++r) acc[jj][r] = C[64 * r + lane];
       }
-      if (DDB) stage_slab_lds(LJ, H, k0, kb, 0, KC, NT, false);
-      for (int kc = 0; kc < k0; kc += KC) {
-        double* S = LJ + (DDB ? ((kc / KC) & 1) * SLABD : 0);
+      // MHE_BIG_ENV: the update starts at the block rows' first nonzero tile column (their
+      // L_Jk left of it are zero), rounded down to a chunk
+      int kst = 0;
+      if (MHE_BIG_ENV && FI) {
+        kst = k0;
+        for (int J = k0; J < kend; ++J) kst = min(kst, FI[J]);
+        kst &= ~(KC - 1);
+      }
+      if (DDB && kst < k0) stage_slab_lds(LJ, H, k0, kb, kst, KC, NT, false);
+      for (int kc = kst; kc < k0; kc += KC) {
+        const int ci = (kc - kst) / KC;  // chunk index: slab buffer ci & 1
+        double* S = LJ + (DDB ? (ci & 1) * SLABD : 0);
         if (DDB) {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this chunk's slab has landed
           __syncthreads();  // ... for every wave; the other buffer's readers are done
-          if (kc + KC < k0) stage_slab_lds(LJ + (((kc / KC) + 1) & 1) * SLABD, H, k0, kb, kc + KC, KC, NT, false);
+          if (kc + KC < k0) stage_slab_lds(LJ + ((ci + 1) & 1) * SLABD, H, k0, kb, kc + KC, KC, NT, false);
         } else {
           __syncthreads();  // the previous slab is consumed
           stage_slab_lds(LJ, H, k0, kb, kc, KC, NT);  // L_Jk, J = k0 + jj, k = kc + kk
@@ -1291,10 +1329,29 @@ __global__ __launch_bounds__(BIG_NTHREADS, BIG_JB == 8 ? 2 : 4) void k_big_chol(
   const int NT = a.NT;
   if (threadIdx.x == 0) *flag = 0;
   init_units(UN);
+  // MHE_BIG_ENV: each tile row's first nonzero tile column from k_big_assemble's component-pair
+  // flags, once per factorization (the first diagonal stage; read by the later stages)
+  const int* FI = MHE_BIG_ENV && SPLIT != 0 ? big_env_first(ws, WL, a.n) : nullptr;
+  if constexpr (MHE_BIG_ENV && SPLIT == 1) {
+    if (kfirst == 0) {
+      const int* EM = big_env_mask(ws, WL);
+      for (int t = threadIdx.x; t < NT; t += BIG_NTHREADS) {
+        const int ca = t / a.NTc;
+        int bm = ca;
+        for (int cb = 0; cb < ca; ++cb) {
+          if (EM[ca * a.n + cb] | EM[cb * a.n + ca]) {
+            bm = cb;
+            break;
+          }
+        }
+        const_cast<int*>(FI)[t] = bm * a.NTc;
+      }
+    }
+  }
   const int kbeg = SPLIT == 1 ? kfirst : 0, kstop = SPLIT == 1 ? big_split_kend(kfirst, NT) : (SPLIT == 2 ? 0 : NT);
   for (int k0 = kbeg; k0 < kstop; k0 += BIG_KB) {
     const int kend = SPLIT == 1 ? kstop : min(k0 + BIG_KB, NT);
-    big_diag_block<BIG_JB, LL, SPLIT != 0>(a, k0, kend, H, LTg, BV, YV, sm, lane, wave);
+    big_diag_block<BIG_JB, LL, SPLIT != 0>(a, k0, kend, H, LTg, BV, YV, sm, lane, wave, FI);
     double* LB = LJ;  // the diagonal block's L_Ik' and L_kk^-T (big_diag_block)
     double* LTs = LJ + BIG_LB_TILES * 256;
     if (*flag) break;
@@ -1475,7 +1532,10 @@ __global__ __launch_bounds__(BIG_NTHREADS, BIG_JB == 8 ? 2 : 4) void k_big_chol(
 #pragma unroll
     for (int m = 0; m < BWD_PF; ++m) {
       const int I = k + 1 + wave + BIG_NW * m;
-      if (I < NT) {
+      if (I < NT && FI && FI[I] > k) {  // outside the envelope (MHE_BIG_ENV): L_Ik = 0, not read
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dst[m][r] = 0.0;
+      } else if (I < NT) {
         const double* L = H + (size_t)big_tile_index(I, k, NT) * 256;
 #pragma unroll
         for (int r = 0; r < 4; ++r)  // L_Ik[tr][bc], k-major tile; coalesced: element (4r + bg) * 16 + bc
@@ -1508,6 +1568,7 @@ __global__ __launch_bounds__(BIG_NTHREADS, BIG_JB == 8 ? 2 : 4) void k_big_chol(
     }
     for (int I = k + 1 + wave + BIG_NW * BWD_PF; I < NT; I += BIG_NW) {  // past the prefetched tiles (C4, C5)
       // (issuing these loads four at a time measured slower: the solve launch 1.23 -> 1.45 ms at C3)
+      if (FI && FI[I] > k) continue;  // outside the envelope
       const double* L = H + (size_t)big_tile_index(I, k, NT) * 256;
       if (MHE_BIG_BWD_COAL) {
         const double dI = yb[16 * I + bc];
@@ -1576,7 +1637,7 @@ __host__ __device__ constexpr int big_rows_lds() { return BIG_LB_TILES * 256 + B
 // k_big_rows.  sm: the LDS region of the slabs, LB and LTs (big_rows_lds() doubles).
 template <int KC, bool DB>
 __device__ __forceinline__ void big_rows_group(double* H, const double* LTg, double* BV, const double* YV,
-                                               double* sm, int NT, int k0, int grp) {
+                                               double* sm, int NT, int k0, int grp, const int* FI = nullptr) {
   static_assert((DB ? 2 : 1) * BIG_KB * KC * 256 <= big_rows_lds(), "the slabs fit the LDS region");
   static_assert(!MHE_BIG_HEAD || KC <= 2, "k0 need not be a multiple of KC: a chunk's tiles must stay below the diagonal");
   double* LB = sm;
@@ -1590,6 +1651,19 @@ __device__ __forceinline__ void big_rows_group(double* H, const double* LTg, dou
   const int I = kend + BIG_NW * grp + wave;
   const bool act = I < NT;
   const int Ic = act ? I : NT - 1;
+  // MHE_BIG_ENV: the group's left-looking update starts at its rows' first nonzero tile
+  // column (rounded down to a chunk); a group whose rows are all zero in this block column
+  // has nothing to do (its tiles hold A_Ik = 0 = L_Ik, and b_I -= L_Ik y_k is no change)
+  int kst = 0;
+  if (MHE_BIG_ENV && FI) {
+    kst = NT;
+    for (int w = 0; w < BIG_NW; ++w) {
+      const int Iw = kend + BIG_NW * grp + w;
+      if (Iw < NT) kst = min(kst, FI[Iw]);
+    }
+    if (kst >= kend) return;
+    kst = min(kst, k0) & ~(KC - 1);
+  }
   d4 acc[BIG_KB];
   constexpr int SLAB = BIG_KB * KC * 256;
   if constexpr (MHE_BIG_ROWS_TLDS && DB) {
@@ -1621,29 +1695,30 @@ __device__ __forceinline__ void big_rows_group(double* H, const double* LTg, dou
       for (int r = 0; r < 4; ++r) acc[kk][r] = A[c * 16 + 4 * r + g];  // A_Ik^T, k-major
     }
   }
-  if (k0 > 0 && !(MHE_BIG_KO & 1)) stage_slab_lds(sm, H, k0, kb, 0, KC, NT, false);
+  if (kst < k0 && !(MHE_BIG_KO & 1)) stage_slab_lds(sm, H, k0, kb, kst, KC, NT, false);
 #if MHE_BIG_ROWS_RPF
   // The row's L_Ik (B operands) a whole chunk ahead: tile kc + kk is loaded into bq[kk]
   // right after chunk kc - KC's MFMAs have read bq[kk], so its HBM latency is covered by
   // a chunk of MFMAs (and the slab wait) instead of by one k step.
   double bq[KC][4];
-  if (k0 > 0 && !(MHE_BIG_KO & 1)) {
+  if (kst < k0 && !(MHE_BIG_KO & 1)) {
 #pragma unroll
     for (int kk = 0; kk < KC; ++kk) {
-      const double* L0 = H + (size_t)big_tile_index(Ic, kk, NT) * 256;
+      const double* L0 = H + (size_t)big_tile_index(Ic, kst + kk, NT) * 256;
 #pragma unroll
       for (int r = 0; r < 4; ++r) bq[kk][r] = L0[64 * r + lane];
     }
   }
-  for (int kc = 0; kc < k0 && !(MHE_BIG_KO & 1); kc += KC) {
-    const double* LJ = sm + (DB ? ((kc / KC) & 1) * SLAB : 0);
-    if (!DB && kc > 0) {
+  for (int kc = kst; kc < k0 && !(MHE_BIG_KO & 1); kc += KC) {
+    const int ci = (kc - kst) / KC;  // chunk index: slab buffer ci & 1 (the first in buffer 0)
+    const double* LJ = sm + (DB ? (ci & 1) * SLAB : 0);
+    if (!DB && kc > kst) {
       __syncthreads();  // the previous chunk's readers are done
       stage_slab_lds(sm, H, k0, kb, kc, KC, NT, false);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this chunk's slab (and row tiles) have landed
     __syncthreads();
-    if (DB && kc + KC < k0) stage_slab_lds(sm + (((kc / KC) + 1) & 1) * SLAB, H, k0, kb, kc + KC, KC, NT, false);
+    if (DB && kc + KC < k0) stage_slab_lds(sm + ((ci + 1) & 1) * SLAB, H, k0, kb, kc + KC, KC, NT, false);
     // a wave without a row (I >= NT: the last group of every launch) skips the MFMAs by a
     // wave-uniform branch around the whole chunk (MHE_BIG_ROWS_SKIP); it still stages and
     // meets the barriers
@@ -1675,19 +1750,20 @@ __device__ __forceinline__ void big_rows_group(double* H, const double* LTg, dou
     }
   }
 #else
-  for (int kc = 0; kc < k0 && !(MHE_BIG_KO & 1); kc += KC) {
-    const double* LJ = sm + (DB ? ((kc / KC) & 1) * SLAB : 0);
-    if (!DB && kc > 0) {
+  for (int kc = kst; kc < k0 && !(MHE_BIG_KO & 1); kc += KC) {
+    const int ci = (kc - kst) / KC;
+    const double* LJ = sm + (DB ? (ci & 1) * SLAB : 0);
+    if (!DB && kc > kst) {
       __syncthreads();  // the previous chunk's readers are done
       stage_slab_lds(sm, H, k0, kb, kc, KC, NT, false);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this chunk's slab has landed
     __syncthreads();  // ... for every wave, and the other buffer's last readers are done
-    if (DB && kc + KC < k0) stage_slab_lds(sm + (((kc / KC) + 1) & 1) * SLAB, H, k0, kb, kc + KC, KC, NT, false);
+    if (DB && kc + KC < k0) stage_slab_lds(sm + ((ci + 1) & 1) * SLAB, H, k0, kb, kc + KC, KC, NT, false);
     double bn[4];
     const double* L0 = H + (size_t)big_tile_index(Ic, kc, NT) * 256;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) bn[r] = L0[64 * r + lane];
+    for (int r = 0; r < 4; ++r) bn[r] = L0[64 * r + lane];  // (kc >= kst)
 #pragma unroll
     for (int kk = 0; kk < KC; ++kk) {
       if (MHE_BIG_HEAD && kc + kk >= k0) break;
@@ -1799,7 +1875,8 @@ __global__ __launch_bounds__(BIG_NTHREADS, 4) void k_big_rows(BigArgs a, int k0)
   const BigWs WL = big_ws_layout(a.P, a.M, a.n, a.NT, a.nz, a.nc);
   double* ws = a.ws + (size_t)b * a.ws_stride;
   extern __shared__ __attribute__((aligned(16))) double sm[];
-  big_rows_group<KC, DB>(ws + WL.H, ws + WL.LT, ws + WL.BV, ws + WL.YV, sm, a.NT, k0, grp);
+  big_rows_group<KC, DB>(ws + WL.H, ws + WL.LT, ws + WL.BV, ws + WL.YV, sm, a.NT, k0, grp,
+                         MHE_BIG_ENV ? big_env_first(ws, WL, a.n) : nullptr);
 }
 
 // ------------------------------------------------------------ border (f4)

@@ -350,6 +350,11 @@ __global__ void k_big_parity_init(BigArgs a, int batch) {
     const bool ok = *(const unsigned long long*)a.cbuf == a.tag;
     a.state[b] = ok ? BIG_RUNNING : MHE_STATUS_BAD_CONSTANTS;
     if (!ok && a.cost) a.cost[b] = NAN;
+    if (MHE_BIG_ENV) {  // the envelope flags k_big_import_hg sets from the caller's system
+      const BigWs WL = big_ws_layout(a.P, a.M, a.n, a.NT, a.nz, a.nc);
+      int* EM = big_env_mask(a.ws + (size_t)b * a.ws_stride, WL);
+      for (int e = 0; e < a.n * a.n; ++e) EM[e] = 0;
+    }
   }
 }
 
@@ -422,8 +427,15 @@ __global__ void k_big_import_hg(BigArgs a, int batch, int ld, const double* Hin,
   const int R = 16 * I + tr, C = 16 * J + tc;  // component-major
   const int r = (R % a.Pp) * a.n + R / a.Pp, c = (C % a.Pp) * a.n + C / a.Pp;
   const int hi = r >= c ? r : c, lo = r >= c ? c : r;  // node-major, lower triangle
-  ws[WL.H + (size_t)blockIdx.x * 256 + threadIdx.x] = Hin[((size_t)b * ld + hi) * ld + lo];
+  const double v = Hin[((size_t)b * ld + hi) * ld + lo];
+  ws[WL.H + (size_t)blockIdx.x * 256 + threadIdx.x] = v;
   if (I == J && tr == 0) ws[WL.BV + 16 * I + tc] = -gin[(size_t)b * ld + (C % a.Pp) * a.n + C / a.Pp];
+  if (MHE_BIG_ENV && __syncthreads_or(v != 0.0) && threadIdx.x == 0) {  // component pair flags (envelope)
+    int* EM = big_env_mask(ws, WL);
+    const int ca = I / a.NTc, cb = J / a.NTc;
+    EM[ca * a.n + cb] = 1;
+    EM[cb * a.n + ca] = 1;
+  }
 }
 
 // The caller's KKT border (rows dp .. dp + K - 1 of a ld = dp + K system, lower part read:
@@ -694,6 +706,25 @@ int32_t mhe_solve_kernel_name(const mhe_dims* dims, int32_t batch, void* stream,
            dims->dyn_model, dims->meas_model, c.sb ? SB_SLOTS : MAX_SLOTS, c.huber ? 1 : 0,
            c.sb ? ", MINW=2, SB=true" : "", c.sb ? " (small-batch factorization: batch <= CUs)" : " (two workgroups per CU)");
   return MHE_OK;
+}
+
+int32_t mhe_big_envelope(const mhe_dims* dims, const void* workspace, size_t workspace_bytes, int32_t traj,
+                         int32_t* first_col, int32_t n_out, void* stream) {
+  int NT = 0;
+  const int rc = check_dims(dims, &NT);
+  if (rc != MHE_OK) return rc;
+  if (!is_big(dims) || !MHE_BIG_ENV) return MHE_ERR_UNSUPPORTED;
+  if (!workspace || !first_col) return MHE_ERR_NULL;
+  if (n_out < NT || traj < 0) return MHE_ERR_DIMS;
+  const BigArgs A = make_big_args(dims, nullptr, NT, const_cast<void*>(workspace));
+  if ((size_t)(traj + 1) * A.ws_stride * sizeof(double) > workspace_bytes) return MHE_ERR_DIMS;
+  const BigWs WL = big_ws_layout(A.P, A.M, A.n, A.NT, A.nz, A.nc);
+  const int* src = (const int*)(A.ws + (size_t)traj * A.ws_stride + WL.ENV) + A.n * A.n;
+  hipStream_t st = (hipStream_t)stream;
+  if (hipMemcpyAsync(first_col, src, (size_t)NT * sizeof(int32_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return MHE_ERR_HIP;
+  return NT;
 }
 
 int32_t mhe_kkt_dim(const mhe_dims* dims) {

@@ -86,6 +86,7 @@ SIGNATURES = {
     "mhe_chol_solve_ws": (ctypes.c_int, [_P, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "mhe_kkt_dim": (c_i32, [_P]),
     "mhe_solve_kernel_name": (c_i32, [_P, c_i32, c_vp, ctypes.c_char_p, c_i32]),
+    "mhe_big_envelope": (c_i32, [_P, c_vp, c_sz, c_i32, c_vp, c_i32, c_vp]),
     "mhe_assemble_kkt_ws": (ctypes.c_int, [_P, c_vp, c_i32, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp,
                                            c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "mhe_ekf_run": (ctypes.c_int, [_PE, c_i32, c_i32, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64,

@@ -141,9 +141,10 @@ def test_integration_stub_declares_the_full_struct():
 
 
 def test_kkt_dim_and_kernel_name_queries_without_gpu():
-    """Host-only ABI v6 queries: mhe_kkt_dim = padded dim + n_extra + n_eq, and
+    """Host-only ABI v6/v7 queries: mhe_kkt_dim = padded dim + n_extra + n_eq, and
     mhe_solve_kernel_name names the instance the launch would pick (batch vs CUs; no
-    device here, so the CU count falls back to 256) or the large-system sequence."""
+    device here, so the CU count falls back to 256) or the large-system sequence;
+    mhe_big_envelope's argument checks (no copy without a workspace)."""
     import numpy as np
     lib = _lib.load()
     d = _lib.MheDims()
@@ -153,8 +154,11 @@ def test_kkt_dim_and_kernel_name_queries_without_gpu():
     assert lib.mhe_solve_kernel_name(d, 1024, None, buf, 256) == 0 and b"two workgroups per CU" in buf.value
     assert lib.mhe_solve_kernel_name(d, 128, None, buf, 256) == 0 and b"SB=true" in buf.value
     assert lib.mhe_solve_kernel_name(d, 128, None, None, 0) == -5  # MHE_ERR_NULL
+    fc = (ctypes.c_int32 * 64)()
+    assert lib.mhe_big_envelope(d, None, 0, 0, fc, 64, None) == -4  # ABI v7: register path, no envelope
     d.N = 500
     assert lib.mhe_solve_kernel_name(d, 8, None, buf, 256) == 0 and buf.value.startswith(b"large-system path")
+    assert lib.mhe_big_envelope(d, None, 0, 0, fc, 64, None) == -5  # no workspace (MHE_ERR_NULL)
     # a bordered problem: equality rows (host pointer) -> dp + n_eq rows
     eq = np.array([[0, 1], [2, 3], [4, -1]], dtype=np.int32)
     d.n_eq = 3

@@ -144,7 +144,7 @@ def test_big_wide_slab_c4_shape_matches_oracle():
     _check_oracle(w, pb, X, cost, iters, status, 2, resolve=None)
 
 
-@pytest.mark.parametrize("cfg", ["c3", "c4"])
+@pytest.mark.parametrize("cfg", ["c3", "c4", "c5"])
 def test_left_and_right_looking_factorizations_agree(cfg):
     """k_big_chol's left-looking block-column update (default) and the right-looking
     trailing update (mhe_set_option(MHE_OPT_BIG_RIGHT_LOOKING, 1), kept for A/B runs)
@@ -152,8 +152,12 @@ def test_left_and_right_looking_factorizations_agree(cfg):
     the same k order (the right-looking form only stores and reloads the partial sums
     between super-blocks, which is exact): iterates after 2 GN steps are bitwise
     identical (C3 reduced N = 60 with the 4-wide instance, C4 full shape with the 8-wide
-    one)."""
-    w = configs.make_c3(B=2, N=60) if cfg == "c3" else configs.make_c4(B=1)
+    one, C5's eight receivers at N = 20, whose component-pair sparsity the split form's
+    envelope skips -- the skipped terms are products with exact zeros)."""
+    if cfg == "c5":
+        w = configs.make_c5(B=2, N=20)
+    else:
+        w = configs.make_c3(B=2, N=60) if cfg == "c3" else configs.make_c4(B=1)
     s = solver.from_workload(w)
     assert s.large_system
     out = {}
