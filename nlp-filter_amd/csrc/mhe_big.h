@@ -311,10 +311,13 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_resid(BigArgs a, int final
   const BigConst CL = big_const_layout(a.P, a.M, n, p, a.nc);
   const BigWs WL = big_ws_layout(a.P, a.M, n, a.NT, a.nz, a.nc);
   double* ws = a.ws + (size_t)b * a.ws_stride;
-  if (MHE_BIG_ENV) {  // the component-pair flags k_big_assemble sets at this iterate
-    int* EM = big_env_mask(ws, WL);
-    for (int t = threadIdx.x; t < n * n; t += BIG_NTHREADS) EM[t] = 0;
-  }
+  // MHE_BIG_ENV: which component pairs (a, b) have a nonzero block of H at this iterate --
+  // from the E, F^T E and G_e values formed below (one coalesced pass over each, flags in
+  // LDS), Qw and Pw; k_big_assemble skips the others' epoch GEMM and writes their tiles as
+  // zeros, the split factorization derives its envelope from them
+  __shared__ int pflag[MHE_BIG_ENV ? n * n : 1];
+  if (MHE_BIG_ENV)
+    for (int t = threadIdx.x; t < n * n; t += BIG_NTHREADS) pflag[t] = 0;
   const double* D = (const double*)(a.cbuf + CL.D);
   const double* Dt = (const double*)(a.cbuf + CL.Dt);
   const double* cw = (const double*)(a.cbuf + CL.cw);
@@ -557,6 +560,24 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_resid(BigArgs a, int final
     a.cost[b] = c;
     if (a.n_bounds > 0) ws[WL.NZ] = COST_NOISE * __DBL_EPSILON__ * z;
   }
+  if (MHE_BIG_ENV && !final_pass) {
+    // (the barrier above ordered every thread's E, F^T E and G_e writes before these reads)
+    const size_t nes = (size_t)n * n * a.P, nge = (size_t)E * n * n;
+    for (size_t t = threadIdx.x; t < nes; t += BIG_NTHREADS) {
+      if (ws[WL.Es + t] != 0.0) pflag[t / a.P] = 1;                     // [(r n + c) P + k]
+      if (ws[WL.FtE + t] != 0.0) pflag[t % (n * n)] = 1;                // [(k n + r) n + c]
+    }
+    for (size_t t = threadIdx.x; t < nge; t += BIG_NTHREADS)
+      if (ws[WL.Ge + t] != 0.0) pflag[t % (n * n)] = 1;                 // [(e n + r) n + c]
+    __syncthreads();
+    int* EM = big_env_mask(ws, WL);
+    for (int t = threadIdx.x; t < n * n; t += BIG_NTHREADS) {
+      const int ca = t / n, cb = t % n, tt = cb * n + ca;
+      const bool nzq = ca == cb || pflag[t] || pflag[tt] || (!a.huber && (Qw[t] != 0.0 || Qw[tt] != 0.0)) ||
+                       (a.has_prior && (Pw[t] != 0.0 || Pw[tt] != 0.0));
+      EM[t] = nzq ? 1 : 0;
+    }
+  }
   if (a.n_bounds > 0 && !final_pass) {
     big_active_set<n>(a, X, ws + WL.BV, (int*)(ws + WL.ACT), red);
     for (int t = threadIdx.x; t < n * a.Pp; t += BIG_NTHREADS) ws[WL.GV + t] = ws[WL.BV + t];  // for the line search
@@ -682,6 +703,12 @@ __global__ __launch_bounds__(256, 4) void k_big_assemble(BigArgs a) {
   const bool live = valid && ch < a.nchl;
   const int q0 = !valid ? 0 : live ? ch * a.pchl : a.nlive + (ch - a.nchl) * BIG_PCH;
   const int np = !valid ? 0 : min(live ? a.pchl : BIG_PCH, (live ? a.nlive : a.npr) - q0);
+  // MHE_BIG_ENV: bit q set when pair q's block of H can be nonzero at this iterate (k_big_resid's
+  // flags); the others skip the epoch GEMM (their G_e are zero) and write zero tiles
+  int lqm = 0;
+#pragma unroll
+  for (int q = 0; q < BIG_PCH; ++q)
+    if (q < np && (!MHE_BIG_ENV || big_env_mask(ws, WL)[a.pa[q0 + q] * n + a.pb[q0 + q]] != 0)) lqm |= 1 << q;
   d4 acc[BIG_PCH];
 #pragma unroll
   for (int q = 0; q < BIG_PCH; ++q) acc[q] = d4{0.0, 0.0, 0.0, 0.0};
@@ -702,7 +729,7 @@ __global__ __launch_bounds__(256, 4) void k_big_assemble(BigArgs a) {
 #pragma unroll
     for (int k = 0; k < NG; ++k) {
       const int g = lane + 64 * k, q = g / KC;
-      gsrc[k] = (g < SGW && q < np && live) ? (a.pa[q0 + q] * n + a.pb[q0 + q]) * 8 : OOB;
+      gsrc[k] = (g < SGW && q < np && live && ((lqm >> q) & 1)) ? (a.pa[q0 + q] * n + a.pb[q0 + q]) * 8 : OOB;
     }
     const int nchk = (E + KC - 1) / KC;
     double sab[NAB], sg[NG];
@@ -757,7 +784,7 @@ __global__ __launch_bounds__(256, 4) void k_big_assemble(BigArgs a) {
             const double a0 = sA[e * 16 + r16], b0 = sB[e * 16 + r16];
 #pragma unroll
             for (int q = 0; q < BIG_PCH; ++q)
-              if (q < np) acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0 * sG[q * KC + e], b0, acc[q], 0, 0, 0);
+              if ((lqm >> q) & 1) acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0 * sG[q * KC + e], b0, acc[q], 0, 0, 0);
           }
         }
       }
@@ -804,7 +831,6 @@ __global__ __launch_bounds__(256, 4) void k_big_assemble(BigArgs a) {
       // E_l[ca][cb] and E_j[cb][ca] (component-major: node index fastest)
       const int sE1 = (int)((WL.Es + (size_t)(ca * n + cb) * P) * 8), sE2 = (int)((WL.Es + (size_t)(cb * n + ca) * P) * 8);
       const int sF = (int)(WL.FtE * 8) + (ca * n + cb) * 8;
-      bool nzv = false;  // any nonzero element in the tile (MHE_BIG_ENV)
       // tile (it, jt) of block (ca, cb) and, off the diagonal pair, its transpose into (jt, it)
 #pragma unroll
       for (int tp = 0; tp < 2; ++tp) {
@@ -818,7 +844,9 @@ __global__ __launch_bounds__(256, 4) void k_big_assemble(BigArgs a) {
           const int tr = tp ? cc : cr, tc = tp ? cr : cc;       // position in the written tile
           const int j = 16 * ti + tr, l = 16 * tj + tc;
           double v;
-          if (j < P && l < P) {
+          if (!((lqm >> q) & 1)) {
+            v = 0.0;  // a pair without a nonzero term (never a diagonal pair: no identity padding)
+          } else if (j < P && l < P) {
             // every operand read along the lane-varying index (l for the tile, j for its
             // transpose): D_lj from D^T or D, D_jl from D or D^T, the exactly symmetric
             // D^T C D either way, E component-major -- coalesced, not P- or n^2-strided
@@ -837,14 +865,8 @@ __global__ __launch_bounds__(256, 4) void k_big_assemble(BigArgs a) {
             const int gr = 16 * I + tr, gc = 16 * J + tc;
             if ((ACT[gr] | ACT[gc]) && gr != gc) v = 0.0;
           }
-          if (MHE_BIG_ENV && tp == 0) nzv |= v != 0.0;
           __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(mhe_u2, v), rh, (tr * 16 + tc) * 8, sT, 0);
         }
-      }
-      if (MHE_BIG_ENV && __builtin_amdgcn_ballot_w64(nzv) != 0 && lane == 0) {
-        int* EM = big_env_mask(ws, WL);  // k_big_resid cleared the flags (plain stores: every writer stores 1)
-        EM[ca * n + cb] = 1;
-        EM[cb * n + ca] = 1;
       }
     }
   }
