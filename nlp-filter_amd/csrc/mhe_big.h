@@ -32,6 +32,12 @@
 #ifndef MHE_BIG_ENV
 #define MHE_BIG_ENV 1  // split form: skip the tiles outside the factor's envelope (component-pair sparsity; C5 5.8x, C3 +8 %)
 #endif
+#ifndef MHE_BIG_WSKIP
+#define MHE_BIG_WSKIP 0  // envelope: a row's wave skips the left-looking chunks left of its own f (rows, diagonal stage; C4 -4 %)
+#endif
+#ifndef MHE_BIG_ASM_ZSKIP
+#define MHE_BIG_ASM_ZSKIP 1  // envelope: k_big_assemble skips storing zero tiles the previous factorization left zero (C5 +2.8 %)
+#endif
 #ifndef MHE_BIG_DIAG_AKPF
 #define MHE_BIG_DIAG_AKPF 1  // diagonal block: the next diagonal tile loaded one column ahead (+0.3 %)
 #endif
@@ -165,6 +171,8 @@ struct BigArgs {
   double huber_delta;
   int border_import;  // k_big_border: the border B, S and r were imported into BM / ZM / KS
                       // (mhe_chol_solve_ws on a KKT system) instead of formed at X
+  int asm_zskip;      // k_big_assemble: tiles left of the envelope the previous iteration's
+                      // factorization used hold zeros (iterations >= 1 of one launch_big)
 };
 
 // measurement weights of trajectory b: the per-solve array when given, else the constants'
@@ -831,6 +839,23 @@ __global__ __launch_bounds__(256, 4) void k_big_assemble(BigArgs a) {
       // E_l[ca][cb] and E_j[cb][ca] (component-major: node index fastest)
       const int sE1 = (int)((WL.Es + (size_t)(ca * n + cb) * P) * 8), sE2 = (int)((WL.Es + (size_t)(cb * n + ca) * P) * 8);
       const int sF = (int)(WL.FtE * 8) + (ca * n + cb) * 8;
+      if (MHE_BIG_ASM_ZSKIP && !((lqm >> q) & 1)) {
+        // a pair without a nonzero term: zero tiles, not stored where the previous
+        // factorization's envelope already left zeros (a tile left of its row's f: A was 0
+        // there, and the factorization wrote nothing but zeros left of f)
+        const int* FIp = big_env_first(ws, WL, n);
+#pragma unroll
+        for (int tp = 0; tp < 2; ++tp) {
+          if (tp == 1 && (ca == cb || it == jt)) break;
+          const int I = ca * NTc + (tp ? jt : it), J = cb * NTc + (tp ? it : jt);
+          if (a.asm_zskip && J < FIp[I]) continue;
+          const int sT = big_tile_index(I, J, a.NT) * 256 * 8;
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(mhe_u2, 0.0), rh, (64 * r + lane) * 8, sT, 0);
+        }
+        continue;
+      }
       // tile (it, jt) of block (ca, cb) and, off the diagonal pair, its transpose into (jt, it)
 #pragma unroll
       for (int tp = 0; tp < 2; ++tp) {
@@ -1082,6 +1107,7 @@ __device__ __forceinline__ void big_diag_block(const BigArgs& a, int k0, int ken
           stage_slab_lds(LJ, H, k0, kb, kc, KC, NT);  // L_Jk, J = k0 + jj, k = kc + kk
           __syncthreads();
         }
+        if (MHE_BIG_WSKIP && FI && act && kc + KC <= FI[Ic]) continue;  // the row's L_Ik here are zero
         // the row's own L_Ik are slab tiles too (I is one of the block's rows J): read from
         // LDS (MHE_BIG_DIAG_LROW) instead of a second time from HBM
         auto lrow = [&](int kk) {
@@ -1686,6 +1712,7 @@ __device__ __forceinline__ void big_rows_group(double* H, const double* LTg, dou
     if (kst >= kend) return;
     kst = min(kst, k0) & ~(KC - 1);
   }
+  const int fI = (MHE_BIG_ENV && MHE_BIG_WSKIP && FI) ? FI[Ic] : 0;  // this wave's row's first nonzero tile column
   d4 acc[BIG_KB];
   constexpr int SLAB = BIG_KB * KC * 256;
   if constexpr (MHE_BIG_ROWS_TLDS && DB) {
@@ -1745,6 +1772,19 @@ __device__ __forceinline__ void big_rows_group(double* H, const double* LTg, dou
     // wave-uniform branch around the whole chunk (MHE_BIG_ROWS_SKIP); it still stages and
     // meets the barriers
     if (MHE_BIG_ROWS_SKIP && !act) continue;
+    if (MHE_BIG_WSKIP && kc + KC <= fI) {
+      // the row's L_Ik of this chunk are zero (left of its f): no MFMAs; the next chunk's
+      // B operands are loaded here when that chunk is the row's first nonzero one
+      if (kc + KC < k0 && kc + 2 * KC > fI) {
+#pragma unroll
+        for (int kk = 0; kk < KC; ++kk) {
+          const double* Ln = H + (size_t)big_tile_index(Ic, kc + KC + kk, NT) * 256;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) bq[kk][r] = Ln[64 * r + lane];
+        }
+      }
+      continue;
+    }
 #pragma unroll
     for (int kk = 0; kk < KC; ++kk) {
       if (MHE_BIG_HEAD && kc + kk >= k0) break;  // k0 odd (MHE_BIG_HEAD): no next chunk either

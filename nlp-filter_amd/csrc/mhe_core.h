@@ -2716,7 +2716,9 @@ int launch_big(const mhe_dims* dm, BigArgs& A, int batch, int max_iter, hipStrea
   const BigAsmShape sh = big_asm_shape(A);
   for (int it = 0; it < max_iter; ++it) {
     if (launch_big_resid<DYN, MEAS>(A, batch, 0, st) != MHE_OK) return MHE_ERR_HIP;
+    A.asm_zskip = it > 0 && cp.split;  // the previous iteration's factorization left its envelope's zeros
     hipLaunchKernelGGL((k_big_assemble<DYN, MEAS>), dim3(sh.blocks, batch), dim3(64 * sh.wpb), sh.lds, st, A);
+    A.asm_zskip = 0;
     launch_big_factor(cp, A, batch, st);
     if (K > 0) hipLaunchKernelGGL((k_big_border<DYN::n, MEAS::p>), dim3(batch), dim3(BIG_NTHREADS), smem_b, st, A);
     if (bounded)
