@@ -2582,14 +2582,14 @@ inline void launch_big_split(const BigCholPlan& p, BigArgs A, int boff, int nb, 
 }
 
 // The second stream and fork / join events of the two-stream split factorization, one set
-// per device, created on first use (nullptr: run on one stream).  SINGLE-CALLER ONLY: two
-// solves enqueued concurrently on different streams of one device would share the fork /
-// join events and could re-record them between another caller's record and wait.  The
-// option is an A/B knob (MHE_BIG_TWO_STREAMS, compiled off); it must stay off in any build
-// that serves concurrent callers.
+// per device, created on first use (nullptr: run on one stream).  Concurrent callers:
+// launch_big_factor holds `use` from its fork record to its join wait, so no other caller
+// re-records the events in between (a stream wait captures the event's last record at
+// enqueue time); their second halves share s2 (serialised, each behind its own fork).
 struct BigAux {
   hipStream_t s2;
   hipEvent_t fork, join;
+  std::mutex use;
 };
 inline BigAux* big_aux(hipStream_t st) {
   static BigAux aux[16];
@@ -2624,6 +2624,7 @@ inline void launch_big_factor(const BigCholPlan& p, const BigArgs& A, int batch,
     launch_big_split(p, A, 0, batch, st);
     return;
   }
+  std::lock_guard<std::mutex> hold(aux->use);  // this caller's record -> wait pairs, uninterleaved
   const int h = ((batch / 2) + 7) & ~7;  // a multiple of 8 (k_big_rows' XCD grouping)
   // the second half starts one diagonal stage behind the first, so that the halves'
   // latency-bound diagonal stages alternate with the other half's row launches
