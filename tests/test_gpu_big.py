@@ -197,3 +197,32 @@ def test_split_factorization_is_batch_invariant():
         assert np.array_equal(a, b)
     for a, b in zip(one, split):
         assert np.array_equal(a, b[5:6])
+
+
+def test_envelope_of_the_eight_receiver_system():
+    """The split factorization's envelope (mhe_big_envelope, ABI v7) is the structure of
+    C5's normal matrix, component by component (N = 20: 2 tiles per component): receiver
+    r's x, y, z rows start at receiver r - 1's x (the range rows to the previous receiver;
+    receiver 0 at column 0), its clock bias b at its own x (pseudoranges), its drift alpha
+    at its own b (dynamics b' = alpha) -- formed on the device from the component pairs
+    k_big_resid finds coupled, so nothing coupled is skipped and nothing uncoupled kept."""
+    import ctypes
+    w = configs.make_c5(B=2, N=20)
+    s = solver.from_workload(w)
+    assert s.large_system
+    s.solve(w.X_init, w.U, w.Y, w.PAR, max_iter=1, tol=0.0)
+    torch.cuda.synchronize()
+    NT = s.lib.mhe_padded_dim(s.dims) // 16
+    NTc = NT // w.n
+    fc = (ctypes.c_int32 * NT)()
+    ws = list(s._ws.values())[-1]
+    nb = s.lib.mhe_workspace_bytes(s.dims, s._chunk(2))
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    assert s.lib.mhe_big_envelope(s.dims, ctypes.c_void_p(ws.data_ptr()), nb, 1, fc, NT, stream) == NT
+    assert s.lib.mhe_big_envelope(s.dims, ctypes.c_void_p(ws.data_ptr()), nb, 2, fc, NT, stream) == -1  # past the batch
+    expect = []
+    for a in range(w.n):
+        r, c = divmod(a, 5)
+        first = (5 * (r - 1) if r > 0 else 0) if c < 3 else (5 * r if c == 3 else 5 * r + 3)
+        expect += [first * NTc] * NTc
+    assert list(fc) == expect
