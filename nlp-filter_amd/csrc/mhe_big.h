@@ -38,6 +38,9 @@
 #ifndef MHE_BIG_ASM_ZSKIP
 #define MHE_BIG_ASM_ZSKIP 1  // envelope: k_big_assemble skips storing zero tiles the previous factorization left zero (C5 +2.8 %)
 #endif
+#ifndef MHE_BIG_RESID_SLOTS
+#define MHE_BIG_RESID_SLOTS 1  // k_big_resid, mixed rows: per-slot gradients (MeasMixed::eval_slots), scratch 752 -> 352 B/lane (C5 +1.8 %)
+#endif
 #ifndef MHE_BIG_DIAG_AKPF
 #define MHE_BIG_DIAG_AKPF 1  // diagonal block: the next diagonal tile loaded one column ahead (+0.3 %)
 #endif
@@ -437,12 +440,13 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_resid(BigArgs a, int final
       double* Gz = ws + WL.GZe + (size_t)e * n * NZX;
       double* Hzz = ws + WL.HZZe + (size_t)e * NZX * NZX;
       double* gz = ws + WL.GZVe + (size_t)e * NZX;
-      double xt[NA];
+      double xt[MHE_BIG_RESID_SLOTS ? 1 : NA];
       for (int c = 0; c < n; ++c) {
-        xt[c] = ws[WL.XE + e * n + c];
+        if (!MHE_BIG_RESID_SLOTS) xt[c] = ws[WL.XE + e * n + c];
         ge[c] = 0.0;
       }
-      for (int c = 0; c < NZX; ++c) xt[n + c] = c < nz ? a.Z[(size_t)b * nz + c] : 0.0;
+      if (!MHE_BIG_RESID_SLOTS)
+        for (int c = 0; c < NZX; ++c) xt[n + c] = c < nz ? a.Z[(size_t)b * nz + c] : 0.0;
       for (int c = 0; c < n * n; ++c) G[c] = 0.0;
       if (nz > 0) {
         for (int c = 0; c < n * NZX; ++c) Gz[c] = 0.0;
@@ -453,6 +457,48 @@ __global__ __launch_bounds__(BIG_NTHREADS) void k_big_resid(BigArgs a, int final
         const double* PR = a.PAR + (long long)b * a.pstride + (long long)i * q;
         const double R = Rw[i];
         if (R == 0.0) continue;  // R = 0 masks the row (empty satellite slot, autonomous-car.py:260-263)
+        if constexpr (MHE_BIG_RESID_SLOTS) {
+          // per-slot gradient: a component in two slots gets their sum (two terms: the same
+          // value as the dense accumulation), zero gradients dropped -- the dense form's
+          // nonzero set; each (ia, ib) entry is still added once per row, so G_e, g_e and
+          // the z blocks take the same values
+          double h, gs[7];
+          int id[7];
+          MEAS::eval_slots([&](int c) { return c < n ? ws[WL.XE + e * n + c] : a.Z[(size_t)b * nz + (c - n)]; }, PR, nz, h,
+                           id, gs);
+#pragma unroll
+          for (int k1 = 0; k1 < 7; ++k1)
+#pragma unroll
+            for (int k2 = k1 + 1; k2 < 7; ++k2)
+              if (id[k1] >= 0 && id[k2] == id[k1]) {
+                gs[k1] += gs[k2];
+                id[k2] = -1;
+              }
+#pragma unroll
+          for (int k1 = 0; k1 < 7; ++k1)
+            if (gs[k1] == 0.0) id[k1] = -1;
+          const double yv = a.Y[(long long)b * a.M + i], ev = yv - h, Re = R * ev;
+          cost += ev * Re;
+          noise += fabs(Re) * (fabs(yv) + fabs(h));
+#pragma unroll
+          for (int u = 0; u < 7; ++u) {
+            if (id[u] < 0) continue;
+            const int ia = id[u];
+            const double ga = gs[u];
+            if (ia < n) ge[ia] += ga * Re;
+            else gz[ia - n] += ga * Re;
+#pragma unroll
+            for (int v = 0; v < 7; ++v) {
+              if (id[v] < 0) continue;
+              const int ib = id[v];
+              const double w2 = ga * R * gs[v];
+              if (ia < n && ib < n) G[ia * n + ib] += w2;
+              else if (ia < n) Gz[ia * NZX + (ib - n)] += w2;
+              else if (ib >= n) Hzz[(ia - n) * NZX + (ib - n)] += w2;
+            }
+          }
+          continue;
+        }
         double h, Gr[NA];
         MEAS::eval(xt, PR, nz, h, Gr);
         const double yv = a.Y[(long long)b * a.M + i], ev = yv - h, Re = R * ev;
@@ -721,7 +767,9 @@ __global__ __launch_bounds__(256, 4) void k_big_assemble(BigArgs a) {
 #pragma unroll
   for (int q = 0; q < BIG_PCH; ++q) acc[q] = d4{0.0, 0.0, 0.0, 0.0};
   const double* Ge = ws + WL.Ge;
-  if (gblock && E > 0) {  // workgroup-uniform
+  // workgroup-uniform; MHE_BIG_ENV: a workgroup none of whose pairs has a nonzero term
+  // skips the whole epoch loop (its staging and barriers, not only the MFMAs)
+  if (gblock && E > 0 && (!MHE_BIG_ENV || __syncthreads_or(lqm != 0))) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     constexpr int KC = BIG_AKC, SA = KC * 16, SGW = BIG_PCH * KC;
     const int SBUF = 2 * SA + WPB * SGW;

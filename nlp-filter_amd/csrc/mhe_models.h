@@ -306,15 +306,34 @@ struct MeasMixed {
 #pragma unroll
     for (int c = 0; c < NA; ++c) G[c] = 0.0;
     int id[7];
+    row_ids(par, nz, id);
+    eval_core([&](int k) { return id[k] >= 0 ? x[id[k]] : 0.0; },
+              [&](int k, double g) {
+                if (id[k] >= 0) G[id[k]] += g;
+              },
+              par, h);
+  }
+  // the row's state / extra-variable index per slot (-1: none or out of range)
+  __device__ static void row_ids(const double* par, int nz, int* id) {
 #pragma unroll
     for (int k = 0; k < 7; ++k) {
       const int v = (int)par[1 + k];
       id[k] = (v >= 0 && v < N_ + nz) ? v : -1;
     }
-    auto X = [&](int k) { return id[k] >= 0 ? x[id[k]] : 0.0; };
-    auto add = [&](int k, double g) {
-      if (id[k] >= 0) G[id[k]] += g;
-    };
+  }
+  // Per-slot form (k_big_resid): the row's values read through xget(index) and its
+  // gradient left per slot, gs[k] = dh/dx[id[k]] (each slot receives one term), so no
+  // array is indexed by a row's data -- the dense x / G arrays of eval() sit in scratch
+  // memory at n = 40.
+  template <class XG>
+  __device__ static void eval_slots(XG xget, const double* par, int nz, double& h, int* id, double* gs) {
+    row_ids(par, nz, id);
+#pragma unroll
+    for (int k = 0; k < 7; ++k) gs[k] = 0.0;
+    eval_core([&](int k) { return id[k] >= 0 ? xget(id[k]) : 0.0; }, [&](int k, double g) { gs[k] += g; }, par, h);
+  }
+  template <class XF, class AF>
+  __device__ static void eval_core(XF X, AF add, const double* par, double& h) {
     const double* v = par + 8;
     switch ((int)par[0]) {
       case MHE_ROW_PSEUDORANGE: {  // nlp/measurements.py:56-70
