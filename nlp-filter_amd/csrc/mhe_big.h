@@ -1427,7 +1427,8 @@ __global__ __launch_bounds__(BIG_NTHREADS, BIG_JB == 8 ? 2 : 4) void k_big_chol(
   init_units(UN);
   // MHE_BIG_ENV: each tile row's first nonzero tile column from k_big_assemble's component-pair
   // flags, once per factorization (the first diagonal stage; read by the later stages)
-  const int* FI = MHE_BIG_ENV && SPLIT != 0 ? big_env_first(ws, WL, a.n) : nullptr;
+  int* FIw = MHE_BIG_ENV && SPLIT != 0 ? big_env_first(ws, WL, a.n) : nullptr;
+  const int* FI = FIw;
   if constexpr (MHE_BIG_ENV && SPLIT == 1) {
     if (kfirst == 0) {
       const int* EM = big_env_mask(ws, WL);
@@ -1440,7 +1441,7 @@ __global__ __launch_bounds__(BIG_NTHREADS, BIG_JB == 8 ? 2 : 4) void k_big_chol(
             break;
           }
         }
-        const_cast<int*>(FI)[t] = bm * a.NTc;
+        FIw[t] = bm * a.NTc;
       }
     }
   }
