@@ -93,7 +93,7 @@ def envelope_share():
     NT = s.lib.mhe_padded_dim(s.dims) // 16
     fc = (ctypes.c_int32 * NT)()
     ws = list(s._ws.values())[-1]
-    nb = s.lib.mhe_workspace_bytes(s.dims, s._chunk(B))
+    nb = ws.numel()
     rc = s.lib.mhe_big_envelope(s.dims, ctypes.c_void_p(ws.data_ptr()), nb, 0, fc, NT,
                                 ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
     if rc < 0:
@@ -110,6 +110,7 @@ res = {"config": cfg, "workload": w.name, "B": B, "iters": it, "d": d, "P": P, "
        "frac_fp64_peak": F * B * it / dt / 1e12 / 78.6,
        "envelope_share": share, "executed_mflop_per_traj_iter": Fx / 1e6,
        "executed_tflops": Fx * B * it / dt / 1e12, "executed_frac": Fx * B * it / dt / 1e12 / 78.6,
-       "workspace_gib": s.lib.mhe_workspace_bytes(s.dims, B) / 2 ** 30, "chunk": s._chunk(B),
+       "workspace_gib": s.lib.mhe_workspace_bytes(s.dims, B) / 2 ** 30,
+       "chunk": s._chunk(B, torch.cuda.current_stream()),  # as solve() sizes it (its own workspace counted free)
        "status": sorted(set(st.tolist()))}
 print(json.dumps(res))
